@@ -1,0 +1,32 @@
+# gsdr-mi355x build: libgsdr.so (HIP, gfx950) and the CPU oracle (plain C, test infrastructure only).
+HIPCC   ?= /opt/rocm/bin/hipcc
+CC      ?= gcc
+ARCH    ?= gfx950
+BUILD   := build
+
+HIPFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -fvisibility=hidden -fvisibility-inlines-hidden \
+            -Wall -Wno-unused-function -Iinclude -Igsdr_amd/csrc -munsafe-fp-atomics
+# Oracle: explicit fmaf where the spec says FMA, no implicit contraction.
+OFLAGS  := -O2 -std=c11 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wextra -Ioracle -mfma
+
+SRCS := $(wildcard gsdr_amd/csrc/*.hip)
+HDRS := $(wildcard gsdr_amd/csrc/*.hpp) $(wildcard include/gsdr/*.h)
+OBJS := $(patsubst gsdr_amd/csrc/%.hip,$(BUILD)/%.o,$(SRCS))
+
+all: gsdr_amd/libgsdr.so oracle/build/liboracle.so
+
+$(BUILD)/%.o: gsdr_amd/csrc/%.hip $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+gsdr_amd/libgsdr.so: $(OBJS)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -Wl,-rpath,/opt/rocm/lib $(OBJS) -o $@
+
+oracle/build/liboracle.so: oracle/gsdr_oracle.c oracle/gsdr_oracle.h
+	@mkdir -p oracle/build
+	$(CC) $(OFLAGS) -shared oracle/gsdr_oracle.c -o $@ -lm -lpthread
+
+clean:
+	rm -rf $(BUILD) gsdr_amd/libgsdr.so oracle/build
+
+.PHONY: all clean

@@ -1,0 +1,301 @@
+#!/usr/bin/env python3
+"""Headline benchmark (BASELINE.json): 127-tap complex<float> FIR, decimate-by-4, 64 M samples per GPU.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+One step = one gsdrFirFC call (the C ABI, through ctypes) over one channel of 67,108,987 complex
+samples resident in HBM -> 2^24 complex outputs. Each rank owns an independent channel (seed
+0x5EED + rank): channels shard across GPUs with no data-path collective, so scaling is weak.
+torch.distributed is used only for the barrier and the max-over-ranks timing reduction.
+
+Rank 0 prints ONE JSON line: value = input samples processed by all ranks / max-over-ranks wall
+time of the K timed steps (Msamples/s), plus a `roofline` object for the FIR kernel (algorithmic
+bytes per launch / mean launch time from HIP events on the launch stream) and a `cpu_baseline`
+object (the C oracle timed on this host, N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Msamples/s + achieved HBM GB/s, 127-tap cplx FIR-dec4, 64M samp, 1/2/4/8 GPU"
+TAPS, DECIM, N_OUT = 127, 4, 1 << 24
+N_IN = (N_OUT - 1) * DECIM + TAPS  # 67,108,987
+ALG_BYTES = 8 * N_IN + 8 * N_OUT + 4 * TAPS  # 671,090,132 B per launch
+ALG_FLOP = 4 * TAPS * N_OUT
+HBM_PEAK_GBPS = 8000.0  # MI355X spec (MI355X_MICROARCH.md); measured copy peak reported alongside
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_fir_fc_d4.json")
+
+
+def dist_env():
+    """(rank, local_rank, world) from the torchrun environment, or a single process."""
+    return (int(os.environ.get("RANK", 0)), int(os.environ.get("LOCAL_RANK", 0)),
+            int(os.environ.get("WORLD_SIZE", 1)))
+
+
+def channel_seed(rank: int) -> int:
+    """Channel c is generated from seed 0x5EED + c (BASELINE config 4: one channel per GPU)."""
+    return 0x5EED + rank
+
+
+def reduce_max(value: float, device) -> float:
+    """Max over ranks (identity when not distributed)."""
+    import torch
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return value
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def barrier():
+    import torch.distributed as dist
+
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.barrier()
+
+
+def aggregate(samples_per_rank: int, world: int, steps: int, seconds_max: float) -> float:
+    """Whole-job Msamples/s: every rank's input samples over the slowest rank's wall time."""
+    return samples_per_rank * world * steps / seconds_max / 1e6
+
+
+def load_pmc_traffic():
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_traffic.py), or None."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            d = json.load(f)
+        return d.get("hbm_bytes_per_launch"), d
+    except (OSError, ValueError):
+        return None, None
+
+
+def measure_copy_peak(torch, device, nbytes=1 << 30, reps=10):
+    a = torch.empty(nbytes // 4, dtype=torch.float32, device=device)
+    b = torch.empty_like(a)
+    a.fill_(1.0)
+    for _ in range(2):
+        b.copy_(a)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e.record()
+    torch.cuda.synchronize()
+    gbps = 2 * nbytes * reps / (s.elapsed_time(e) * 1e-3) / 1e9
+    del a, b
+    return gbps
+
+
+def cpu_baseline(x_host, taps_np, threads):
+    """Time the C oracle (oracle/gsdr_oracle.c, scalar fmaf port of fir.cu:49-71) on this host."""
+    import numpy as np
+
+    from oracle import oracle as orc
+
+    best = float("inf")
+    for _ in range(3):
+        t0 = time.perf_counter()
+        orc.fir_fc_mt(taps_np, x_host, DECIM, N_OUT, threads)
+        best = min(best, time.perf_counter() - t0)
+    # single-thread rate on a 1/16 slice of the same workload
+    n1 = N_OUT // 16
+    xs = np.ascontiguousarray(x_host[: (n1 - 1) * DECIM + TAPS])
+    t0 = time.perf_counter()
+    orc.fir_fc_mt(taps_np, xs, DECIM, n1, 1)
+    t1 = time.perf_counter() - t0
+    return {
+        "value": round(N_IN / best / 1e6, 2),
+        "unit": "Msamples/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"full config-2 channel ({N_IN} input samples -> {N_OUT} outputs), best of 3, "
+                  f"{threads} threads (static split by output range)",
+        "single_thread_msamples_per_s": round(((n1 - 1) * DECIM + TAPS) / t1 / 1e6, 2),
+    }
+
+
+def secondary_configs(torch, ops, device, taps):
+    """Config 3 (fused NCO + FIR + FM, 64 M samples) and config 5 (QPSK256 16 M symbols): kernel
+    times from HIP events, reported beside the headline line."""
+    import numpy as np
+
+    out = {}
+    fs, tune, chan, dev_hz = 1.0e6, 0.0, 1.0e5, 2.0e4
+    n_fm = (1 << 24) - 1
+    g = torch.Generator(device=device).manual_seed(0x5EED)
+    x = (torch.rand(2 * (n_fm * DECIM + TAPS), device=device, generator=g) * 2 - 1).view(torch.complex64)
+    y = torch.empty(n_fm, dtype=torch.float32, device=device)
+    for _ in range(3):
+        ops.fm_demod(x, taps, fs, tune, chan, dev_hz, DECIM, 0, n_fm, out=y)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 10
+    s.record()
+    for _ in range(reps):
+        ops.fm_demod(x, taps, fs, tune, chan, dev_hz, DECIM, 0, n_fm, out=y)
+    e.record()
+    torch.cuda.synchronize()
+    t = s.elapsed_time(e) / reps * 1e-3
+    b = 8 * x.numel() + 4 * n_fm + 4 * TAPS
+    out["fm_chain"] = {"config": "NCO + 127-tap FIR (D=4) + FM discriminator, 67,108,987 samples",
+                       "us_per_launch": round(t * 1e6, 2), "msamples_per_s": round(x.numel() / t / 1e6, 1),
+                       "alg_gbps": round(b / t / 1e9, 1)}
+    del x, y
+    n = 1 << 24
+    ops.qpsk256_init(0, 1.0, device.index)
+    syms = torch.randint(0, 256, (n,), dtype=torch.uint8, device=device, generator=g)
+    tx = torch.empty(n, dtype=torch.complex64, device=device)
+    rx_bytes = torch.empty(n, dtype=torch.uint8, device=device)
+    ops.qpsk256_modulate(syms, 0, out=tx)
+    rx = tx + torch.randn(n, dtype=torch.complex64, device=device, generator=g) * (0.02 * np.sqrt(2.0))
+    for _ in range(2):
+        ops.qpsk256_modulate(syms, 0, out=tx)
+        ops.qpsk256_demodulate(rx, 0, out=rx_bytes)
+    s1, e1, s2, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(4))
+    s1.record()
+    for _ in range(reps):
+        ops.qpsk256_modulate(syms, 0, out=tx)
+    e1.record()
+    s2.record()
+    for _ in range(reps):
+        ops.qpsk256_demodulate(rx, 0, out=rx_bytes)
+    e2.record()
+    torch.cuda.synchronize()
+    tm, td = s1.elapsed_time(e1) / reps * 1e-3, s2.elapsed_time(e2) / reps * 1e-3
+    out["qpsk256"] = {"config": "QPSK256 rectangular, 2^24 symbols, AWGN sigma 0.02/axis",
+                      "modulate_us": round(tm * 1e6, 2), "demodulate_us": round(td * 1e6, 2),
+                      "alg_gbps_mod": round(9 * n / tm / 1e9, 1), "alg_gbps_demod": round(9 * n / td / 1e9, 1),
+                      "ser": round(float((rx_bytes != syms).float().mean()), 6)}
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--variant", type=int, default=-1, help="FC/D=4 tile shape (gsdrxFirFCVariant), -1 = default")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    rank, local_rank, world = dist_env()
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            sys.exit("--gpus N > 1 must be launched with torch.distributed.run (one process per GPU)")
+        raise SystemExit(f"WORLD_SIZE={world} does not match --gpus {args.gpus}")
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    from gsdr_amd import ops
+    from gsdr_amd.signals import lowpass_taps
+
+    taps_np = lowpass_taps(TAPS, 0.1)
+    taps = torch.from_numpy(taps_np).to(device)
+    g = torch.Generator(device=device).manual_seed(channel_seed(rank))
+    x = (torch.rand(2 * N_IN, device=device, generator=g) * 2 - 1).view(torch.complex64)
+    y = torch.empty(N_OUT, dtype=torch.complex64, device=device)
+
+    def step():
+        if args.variant >= 0:
+            ops.fir_variant(args.variant, taps, x, DECIM, N_OUT, out=y)
+        else:
+            ops.fir(taps, x, DECIM, N_OUT, out=y)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    barrier()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        starts[k].record()  # torch's current stream == the stream gsdrFirFC is launched on
+        step()
+        ends[k].record()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    barrier()
+    wall_max = reduce_max(wall, device)
+    kern_s = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / args.steps * 1e-3
+    kern_s_max = reduce_max(kern_s, device)
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    value = aggregate(N_IN, world, args.steps, wall_max)
+    achieved = ALG_BYTES / kern_s / 1e9
+    traffic, pmc = load_pmc_traffic()
+    line = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "Msamples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(wall_max / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: I/Q uniform[-1,1) complex64 per channel (torch generator seed 0x5EED + rank), "
+                "127-tap Hamming-windowed sinc low-pass, fc = 0.1 fs",
+        "config": {"workload": "127-tap complex<float> FIR decimate-by-4, 64M samples per GPU (BASELINE configs[1])",
+                   "taps": TAPS, "decimation": DECIM, "input_samples": N_IN, "outputs": N_OUT,
+                   "channels": world, "parallelism": f"independent channels, 1 per GPU x {world}",
+                   "entry_point": "gsdrFirFC" if args.variant < 0 else f"gsdrxFirFCVariant({args.variant})"},
+        "achieved_hbm_gbps": round(achieved, 1),
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 4),
+            "traffic": traffic,
+            "kernel": "k_fir_poly<float, float2, D=4, R=8, JC=16, WG=128>",
+            "alg_bytes_per_launch": ALG_BYTES,
+            "kernel_us_mean": round(kern_s * 1e6, 2),
+            "kernel_us_max_over_ranks": round(kern_s_max * 1e6, 2),
+            "alg_tflops": round(ALG_FLOP / kern_s / 1e12, 2),
+        },
+    }
+    if pmc:
+        line["roofline"]["traffic_source"] = os.path.relpath(PMC_SUMMARY, ROOT)
+    try:
+        cp = measure_copy_peak(torch, device)
+        line["roofline"]["measured_copy_gbps"] = round(cp, 1)
+        line["roofline"]["frac_of_measured_copy"] = round(achieved / cp, 4)
+    except RuntimeError:
+        pass
+    if world == 1 and not args.no_secondary:
+        line["secondary"] = secondary_configs(torch, ops, device, taps)
+    if world == 1 and not args.no_cpu_baseline:
+        threads = min(16, os.cpu_count() or 1)
+        line["cpu_baseline"] = cpu_baseline(x.cpu().numpy(), taps_np, threads)
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

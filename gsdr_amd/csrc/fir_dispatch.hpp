@@ -1,0 +1,169 @@
+// gsdr-mi355x: host-side choice of FIR kernel instantiation for a job (FIR, FM chain or AM chain).
+//
+// Fast paths (tiled, LDS-staged, register-windowed; see fir_engine.hpp):
+//   complex input: D in {2, 4, 8} polyphase kernel, D == 1 contiguous-window kernel
+//   real input:    D in {4, 8}    polyphase kernel, D in {1, 2} contiguous-window kernel
+// Everything else (other decimations, tap spans that would not fit the LDS budget) runs the generic
+// one-output-per-thread kernel, which is correct for any shape.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <type_traits>
+
+#include "fir_engine.hpp"
+#include "launch.hpp"
+
+namespace gsdr {
+
+struct FirJob {
+  const void* in = nullptr;
+  const void* taps = nullptr;
+  void* out = nullptr;
+  size_t D = 1;
+  size_t T = 0;
+  size_t N = 0;  // outputs written
+  size_t L = 0;  // input samples readable
+  int mode = kModeFir;
+  int variant = -1;  // FC / D=4 tile-shape override for tuning (-1 = default)
+  uint32_t nco_inc = 0;
+  uint32_t nco_n0 = 0;
+  float fm_gain = 0.0f;
+};
+
+// LDS budget per workgroup for the tiled kernels (keeps >= 2 workgroups per CU on 160 KiB).
+constexpr size_t kMaxTileLds = 64 * 1024;
+
+inline FirParams make_params(const FirJob& j) {
+  FirParams p{};
+  p.in = j.in;
+  p.taps = j.taps;
+  p.out = j.out;
+  p.L = j.L;
+  p.N = j.N;
+  p.T = (uint32_t)j.T;
+  p.D = (uint32_t)j.D;
+  p.nco_inc = j.nco_inc;
+  p.nco_n0 = j.nco_n0;
+  p.fm_gain = j.fm_gain;
+  return p;
+}
+
+template <class TapT, class InT, int MODE>
+hipError_t launch_generic(const FirJob& j, hipStream_t s) {
+  FirParams p = make_params(j);
+  const uint64_t blocks = ceil_div<uint64_t>(j.N, 256);
+  if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
+  k_fir_generic<TapT, InT, MODE><<<dim3((uint32_t)blocks), dim3(256), 0, s>>>(p);
+  return launch_status();
+}
+
+template <class TapT, class InT, int D, int R, int JC, int WG, int MODE>
+hipError_t launch_poly(const FirJob& j, hipStream_t s) {
+  using Geo = TileGeo<InT, D, R, WG>;
+  FirParams p = make_params(j);
+  const uint64_t rows = ceil_div<uint64_t>(j.T, (uint64_t)D);
+  const uint64_t nch = ceil_div<uint64_t>(rows, (uint64_t)JC);
+  const uint64_t span = nch * JC * D;
+  if (span > 0x40000000ull) return launch_generic<TapT, InT, MODE>(j, s);
+  const size_t lds = poly_lds_bytes<InT, D, R, WG>((uint32_t)span, MODE);
+  if (lds > kMaxTileLds) return launch_generic<TapT, InT, MODE>(j, s);
+  p.nch = (uint32_t)nch;
+  const uint32_t stride = (MODE == kModeFm) ? Geo::KT - 1 : Geo::KT;
+  p.tile_stride = stride;
+  const uint64_t tiles = ceil_div<uint64_t>(j.N, stride);
+  if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
+  const bool vec = aligned16(j.in) && ((uint64_t)stride * D * sizeof(InT)) % 16 == 0;
+  if (vec) {
+    k_fir_poly<TapT, InT, D, R, JC, WG, true, MODE><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
+  } else {
+    k_fir_poly<TapT, InT, D, R, JC, WG, false, MODE><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
+  }
+  return launch_status();
+}
+
+template <class TapT, class InT, int D, int R, int IC, int WG, int MODE>
+hipError_t launch_contig(const FirJob& j, hipStream_t s) {
+  using Geo = TileGeo<InT, D, R, WG>;
+  FirParams p = make_params(j);
+  const uint64_t nch = ceil_div<uint64_t>(j.T, (uint64_t)IC);
+  const uint64_t span = nch * IC;
+  if (span > 0x40000000ull) return launch_generic<TapT, InT, MODE>(j, s);
+  const size_t lds = poly_lds_bytes<InT, D, R, WG>((uint32_t)span, MODE);
+  if (lds > kMaxTileLds) return launch_generic<TapT, InT, MODE>(j, s);
+  p.nch = (uint32_t)nch;
+  const uint32_t stride = (MODE == kModeFm) ? Geo::KT - 1 : Geo::KT;
+  p.tile_stride = stride;
+  const uint64_t tiles = ceil_div<uint64_t>(j.N, stride);
+  if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
+  const bool vec = aligned16(j.in) && ((uint64_t)stride * D * sizeof(InT)) % 16 == 0;
+  if (vec) {
+    k_fir_contig<TapT, InT, D, R, IC, WG, true, MODE><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
+  } else {
+    k_fir_contig<TapT, InT, D, R, IC, WG, false, MODE><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
+  }
+  return launch_status();
+}
+
+// Tile-shape variants of the headline case (real taps, complex input, D = 4), selectable through
+// gsdrxFirFCVariant for tuning sweeps. Variant 0 is the default.
+template <class TapT, class InT, int MODE>
+hipError_t launch_d4_complex(const FirJob& j, hipStream_t s) {
+  switch (j.variant) {
+    case 1:
+      return launch_poly<TapT, InT, 4, 4, 16, 256, MODE>(j, s);
+    case 2:
+      return launch_poly<TapT, InT, 4, 8, 16, 256, MODE>(j, s);
+    case 3:
+      return launch_poly<TapT, InT, 4, 8, 16, 64, MODE>(j, s);
+    case 4:
+      return launch_poly<TapT, InT, 4, 8, 32, 128, MODE>(j, s);
+    case 5:
+      return launch_poly<TapT, InT, 4, 4, 8, 256, MODE>(j, s);
+    case 6:
+      return launch_poly<TapT, InT, 4, 16, 16, 128, MODE>(j, s);
+    case 7:
+      return launch_generic<TapT, InT, MODE>(j, s);
+    default:
+      return launch_poly<TapT, InT, 4, 8, 16, 128, MODE>(j, s);
+  }
+}
+
+template <class TapT, class InT, int MODE>
+hipError_t launch_fir(const FirJob& j, hipStream_t s) {
+  constexpr bool kComplexIn = SampleT<InT>::kPerGranule == 2;
+  // the tiled kernels address taps through a 32-bit buffer descriptor
+  if (j.T > (1u << 26)) return launch_generic<TapT, InT, MODE>(j, s);
+  if constexpr (kComplexIn) {
+    switch (j.D) {
+      case 1:
+        return launch_contig<TapT, InT, 1, 8, 16, 256, MODE>(j, s);
+      case 2:
+        return launch_poly<TapT, InT, 2, 8, 16, 128, MODE>(j, s);
+      case 4:
+        if constexpr (MODE == kModeFir && std::is_same<TapT, float>::value) {
+          if (j.variant >= 0) return launch_d4_complex<TapT, InT, MODE>(j, s);
+        }
+        return launch_poly<TapT, InT, 4, 8, 16, 128, MODE>(j, s);
+      case 8:
+        return launch_poly<TapT, InT, 8, 8, 8, 128, MODE>(j, s);
+      default:
+        return launch_generic<TapT, InT, MODE>(j, s);
+    }
+  } else {
+    switch (j.D) {
+      case 1:
+        return launch_contig<TapT, InT, 1, 16, 32, 256, MODE>(j, s);
+      case 2:
+        return launch_contig<TapT, InT, 2, 8, 16, 256, MODE>(j, s);
+      case 4:
+        return launch_poly<TapT, InT, 4, 8, 8, 128, MODE>(j, s);
+      case 8:
+        return launch_poly<TapT, InT, 8, 8, 8, 128, MODE>(j, s);
+      default:
+        return launch_generic<TapT, InT, MODE>(j, s);
+    }
+  }
+}
+
+}  // namespace gsdr

@@ -1,0 +1,476 @@
+// gsdr-mi355x: the decimating-FIR engine behind gsdrFir*, gsdrFmDemod and gsdrAmDemod.
+//
+// What it computes (reference src/fir.cu:26-71):
+//     y[k] = sum_{i<T} x[k*D + i] * t[i]
+// optionally with an NCO mix applied to x first (reference src/adjustFrequency.cu:25-56, re-specified in
+// SURVEY.md App. A.3) and a demodulator epilogue (FM: reference src/fm.cu:59-68, AM: src/am.cu:49).
+//
+// How (MI355X / gfx950, wave64, 160 KiB LDS per CU):
+//   * One workgroup owns a tile of KT = WG * R consecutive outputs. It stages the tile's input span
+//     (KT*D + taps samples) from HBM into LDS with 16-byte loads (one "granule" = 2 complex or 4 real
+//     samples); the NCO mix, when present, is applied once per staged sample on the way in.
+//   * Each thread then computes R consecutive outputs from a register-resident sliding window read out
+//     of LDS with ds_read_b128, so each staged sample is read from LDS ~(R+JC-1)/R times instead of
+//     T/D times. Taps are wave-uniform: they are read with scalar loads straight into SGPR operands of
+//     the FMAs (no VGPRs, no LDS traffic for taps).
+//   * Decimation D that is a multiple of the granule width is handled polyphase: a granule holds G
+//     consecutive phases of one input "row" (D samples), and the window for one granule column only
+//     carries the phases that meet the taps t[j*D + h*G + e] in flight -- no wasted window registers.
+//   * A thread's segment is SG granules; when SG is even a one-granule pad is inserted after each
+//     segment so the per-lane stride is odd and the 16-lane groups of ds_read_b128 are bank-conflict
+//     free, while every window offset stays a compile-time constant.
+//   * No MFMA: 12.7 flop/byte at T=127, D=4 is an HBM-bound 1-D correlation.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace gsdr {
+
+// ------------------------------------------------------------------------------------------------
+// Sample and product types
+// ------------------------------------------------------------------------------------------------
+template <class T>
+struct SampleT;
+template <>
+struct SampleT<float> {
+  static constexpr int kPerGranule = 4;
+};
+template <>
+struct SampleT<float2> {
+  static constexpr int kPerGranule = 2;
+};
+
+template <class TapT, class InT>
+struct Product {
+  using type = float2;
+};
+template <>
+struct Product<float, float> {
+  using type = float;
+};
+
+__device__ __forceinline__ void set_zero(float& a) { a = 0.0f; }
+__device__ __forceinline__ void set_zero(float2& a) { a = make_float2(0.0f, 0.0f); }
+
+// Element e (compile-time after unrolling) of a 16-byte granule.
+template <class InT>
+__device__ __forceinline__ InT granule_sample(const float4& g, int e);
+template <>
+__device__ __forceinline__ float granule_sample<float>(const float4& g, int e) {
+  return e == 0 ? g.x : (e == 1 ? g.y : (e == 2 ? g.z : g.w));
+}
+template <>
+__device__ __forceinline__ float2 granule_sample<float2>(const float4& g, int e) {
+  return e == 0 ? make_float2(g.x, g.y) : make_float2(g.z, g.w);
+}
+
+// acc += x * t, with the component products of the reference's cuComplex operator overloads
+// (reference src/cuComplexOperatorOverloads.cuh:25-33: c*r, r*c, cuCmulf).
+__device__ __forceinline__ void mac(float& acc, float x, float t) { acc = fmaf(x, t, acc); }
+__device__ __forceinline__ void mac(float2& acc, float2 x, float t) {
+  acc.x = fmaf(x.x, t, acc.x);
+  acc.y = fmaf(x.y, t, acc.y);
+}
+__device__ __forceinline__ void mac(float2& acc, float x, float2 t) {
+  acc.x = fmaf(t.x, x, acc.x);
+  acc.y = fmaf(t.y, x, acc.y);
+}
+__device__ __forceinline__ void mac(float2& acc, float2 x, float2 t) {
+  acc.x = fmaf(x.x, t.x, acc.x);
+  acc.x = fmaf(-x.y, t.y, acc.x);
+  acc.y = fmaf(x.x, t.y, acc.y);
+  acc.y = fmaf(x.y, t.x, acc.y);
+}
+
+// Taps are fetched with scalar buffer loads (s_buffer_load_dword{,x2,x4,x8}) through a buffer
+// descriptor whose range is exactly the caller's T taps: the hardware range check returns 0 for the
+// zero-padding past T, so no clamp/select instructions are needed and the tap lands directly in the
+// SGPR operand of v_pk_fma_f32 (broadcast with op_sel_hi).
+typedef int gsdr_v4i32 __attribute__((ext_vector_type(4)));
+__device__ float gsdr_s_buffer_load_f32(gsdr_v4i32 rsrc, int offset, int aux) __asm("llvm.amdgcn.s.buffer.load.f32");
+
+struct TapBuf {
+  gsdr_v4i32 rsrc;
+};
+
+__device__ __forceinline__ TapBuf make_tapbuf(const void* taps, uint32_t bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(taps);
+  TapBuf b;
+  b.rsrc = gsdr_v4i32{(int)(uint32_t)a, (int)(uint32_t)(a >> 32) & 0xffff, (int)bytes, 0x00020000};
+  return b;
+}
+
+template <class TapT>
+__device__ __forceinline__ TapT tap_at(const TapBuf& tb, uint32_t idx);
+template <>
+__device__ __forceinline__ float tap_at<float>(const TapBuf& tb, uint32_t idx) {
+  return gsdr_s_buffer_load_f32(tb.rsrc, (int)(idx * 4u), 0);
+}
+template <>
+__device__ __forceinline__ float2 tap_at<float2>(const TapBuf& tb, uint32_t idx) {
+  return make_float2(gsdr_s_buffer_load_f32(tb.rsrc, (int)(idx * 8u), 0),
+                     gsdr_s_buffer_load_f32(tb.rsrc, (int)(idx * 8u + 4u), 0));
+}
+
+// ------------------------------------------------------------------------------------------------
+// Launch parameters (one struct for every mode; passed by value)
+// ------------------------------------------------------------------------------------------------
+enum Mode : int { kModeFir = 0, kModeFm = 1, kModeAm = 2 };
+
+struct FirParams {
+  const void* in;
+  const void* taps;
+  void* out;
+  uint64_t L;            // input samples readable
+  uint64_t N;            // outputs to write
+  uint32_t T;            // tap count (>= 1)
+  uint32_t nch;          // tap chunks per phase column
+  uint32_t tile_stride;  // outputs advanced per tile (KT, or KT - 1 for the FM discriminator)
+  uint32_t D;            // decimation (used by the generic kernel)
+  uint32_t nco_inc;      // NCO phase increment per sample, 2^-32 cycles
+  uint32_t nco_n0;       // low 32 bits of firstSampleIndex
+  float fm_gain;         // FM discriminator gain
+  uint32_t pad_;
+};
+
+// ------------------------------------------------------------------------------------------------
+// NCO: exact integer phase, float sincospi.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ float2 nco_mix(float2 x, uint32_t phase) {
+  float sn, cs;
+  // phase / 2^32 cycles == (int32)phase / 2^31 half-cycles, in [-1, 1)
+  sincospif((float)(int32_t)phase * 0x1p-31f, &sn, &cs);
+  return make_float2(x.x * cs - x.y * sn, x.x * sn + x.y * cs);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Tile geometry
+// ------------------------------------------------------------------------------------------------
+template <class InT, int D, int R, int WG>
+struct TileGeo {
+  static constexpr int G = SampleT<InT>::kPerGranule;
+  static_assert((R * D) % G == 0, "a thread segment must be whole granules");
+  static constexpr int SG = R * D / G;             // granules per thread segment
+  static constexpr int PAD = (SG % 2 == 0) ? 1 : 0;  // odd lane stride -> conflict-free ds_read_b128
+  static constexpr int SGP = SG + PAD;
+  static constexpr int KT = WG * R;                  // outputs per tile
+  __host__ __device__ static constexpr uint32_t padded(uint32_t g) { return g + PAD * (g / SG); }
+};
+
+// 16 bytes = G consecutive samples starting at s; samples at or past L read as zero.
+template <class InT, bool VEC>
+__device__ __forceinline__ float4 load_granule(const InT* __restrict__ in, uint64_t s, uint64_t L) {
+  constexpr int G = SampleT<InT>::kPerGranule;
+  if (VEC && s + G <= L) {
+    return *reinterpret_cast<const float4*>(in + s);
+  }
+  float4 r = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  if constexpr (G == 2) {
+    if (s < L) {
+      const float2 a = reinterpret_cast<const float2*>(in)[s];
+      r.x = a.x;
+      r.y = a.y;
+    }
+    if (s + 1 < L) {
+      const float2 b = reinterpret_cast<const float2*>(in)[s + 1];
+      r.z = b.x;
+      r.w = b.y;
+    }
+  } else {
+    const float* f = reinterpret_cast<const float*>(in);
+    if (s < L) r.x = f[s];
+    if (s + 1 < L) r.y = f[s + 1];
+    if (s + 2 < L) r.z = f[s + 2];
+    if (s + 3 < L) r.w = f[s + 3];
+  }
+  return r;
+}
+
+template <class InT, int MODE>
+__device__ __forceinline__ float4 stage_transform(float4 v, uint64_t s, const FirParams& p) {
+  if constexpr (MODE != kModeFir) {
+    static_assert(SampleT<InT>::kPerGranule == 2, "NCO modes take complex input");
+    const uint32_t n = p.nco_n0 + (uint32_t)s;  // absolute sample index mod 2^32
+    const float2 a = nco_mix(make_float2(v.x, v.y), n * p.nco_inc);
+    const float2 b = nco_mix(make_float2(v.z, v.w), (n + 1u) * p.nco_inc);
+    v = make_float4(a.x, a.y, b.x, b.y);
+  }
+  return v;
+}
+
+// Stage granules [0, NG) of the tile starting at global sample S0 into LDS (padded layout).
+// The first SG*WG granules (the tile body) are loaded fully unrolled so every HBM load is in flight
+// before the first LDS write; the remaining halo granules follow in a short strided loop.
+template <class InT, class Geo, int WG, bool VEC, int MODE>
+__device__ __forceinline__ void stage_tile(float4* __restrict__ lds, const InT* __restrict__ in, uint64_t S0,
+                                           uint32_t NG, const FirParams& p) {
+  constexpr int G = Geo::G;
+  // at most 8 granules (128 B) in flight per lane: bounds the staging registers for large segments
+  constexpr int SB = Geo::SG < 8 ? Geo::SG : 8;
+  static_assert(Geo::SG % SB == 0, "segment granules must split into whole staging batches");
+  const uint32_t tid = threadIdx.x;
+  // wave-uniform: is the whole staged span readable? (every tile but the last)
+  const bool whole = VEC && (S0 + (uint64_t)NG * G <= p.L);
+#pragma unroll
+  for (int b0 = 0; b0 < Geo::SG; b0 += SB) {
+    float4 v[SB];
+    if (whole) {
+      const float4* __restrict__ src = reinterpret_cast<const float4*>(in + S0);
+#pragma unroll
+      for (int k = 0; k < SB; ++k) v[k] = src[(b0 + k) * WG + tid];
+    } else {
+#pragma unroll
+      for (int k = 0; k < SB; ++k) {
+        v[k] = load_granule<InT, VEC>(in, S0 + (uint64_t)((b0 + k) * WG + tid) * G, p.L);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < SB; ++k) {
+      const uint32_t g = (b0 + k) * WG + tid;
+      lds[Geo::padded(g)] = stage_transform<InT, MODE>(v[k], S0 + (uint64_t)g * G, p);
+    }
+  }
+  for (uint32_t g = Geo::SG * WG + tid; g < NG; g += WG) {
+    const uint64_t s = S0 + (uint64_t)g * G;
+    lds[Geo::padded(g)] = stage_transform<InT, MODE>(load_granule<InT, VEC>(in, s, p.L), s, p);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Epilogues
+// ------------------------------------------------------------------------------------------------
+template <class OutT, int R>
+__device__ __forceinline__ void store_fir(OutT* __restrict__ out, uint64_t k0, uint64_t N, const OutT (&acc)[R]) {
+  constexpr int PER16 = 16 / sizeof(OutT);
+  static_assert(R % PER16 == 0, "R must fill whole 16-byte stores");
+  if (k0 + R <= N && (reinterpret_cast<uintptr_t>(out + k0) & 15u) == 0) {
+    float4* o = reinterpret_cast<float4*>(out + k0);
+#pragma unroll
+    for (int q = 0; q < R / PER16; ++q) {
+      float4 w;
+      if constexpr (PER16 == 2) {
+        w = make_float4(reinterpret_cast<const float2&>(acc[2 * q]).x, reinterpret_cast<const float2&>(acc[2 * q]).y,
+                        reinterpret_cast<const float2&>(acc[2 * q + 1]).x,
+                        reinterpret_cast<const float2&>(acc[2 * q + 1]).y);
+      } else {
+        w = make_float4(reinterpret_cast<const float&>(acc[4 * q]), reinterpret_cast<const float&>(acc[4 * q + 1]),
+                        reinterpret_cast<const float&>(acc[4 * q + 2]),
+                        reinterpret_cast<const float&>(acc[4 * q + 3]));
+      }
+      o[q] = w;
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (k0 + r < N) out[k0 + r] = acc[r];
+    }
+  }
+}
+
+// FM discriminator of consecutive FIR outputs: g * arg(y1 * conj(y0)) (reference src/fm.cu:66-68,
+// src/quad_demod.cu:30-31).
+__device__ __forceinline__ float fm_disc(float2 y0, float2 y1, float g) {
+  const float re = y1.x * y0.x + y1.y * y0.y;
+  const float im = y1.y * y0.x - y1.x * y0.y;
+  return g * atan2f(im, re);
+}
+
+// AM envelope: 2 * saturate(|y|) - 1, saturate(NaN) = 0 (reference src/am.cu:49, quad_demod.cu:47-48).
+__device__ __forceinline__ float am_env(float2 y) {
+  float m = hypotf(y.x, y.y);
+  m = (m > 0.0f) ? (m < 1.0f ? m : 1.0f) : 0.0f;
+  return 2.0f * m - 1.0f;
+}
+
+// Shared by both tiled kernels. `xs` is a WG-sized LDS exchange area (FM mode only).
+template <int MODE, class OutT, int R, int WG>
+__device__ __forceinline__ void tile_epilogue(const FirParams& p, uint64_t out0, OutT (&acc)[R], float2* xs) {
+  const uint32_t t = threadIdx.x;
+  const uint32_t local0 = t * R;
+  if constexpr (MODE == kModeFir) {
+    store_fir<OutT, R>(reinterpret_cast<OutT*>(p.out), out0 + local0, p.N, acc);
+  } else if constexpr (MODE == kModeAm) {
+    float* out = reinterpret_cast<float*>(p.out);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint64_t m = out0 + local0 + r;
+      if (m < p.N) out[m] = am_env(acc[r]);
+    }
+  } else {
+    // Tiles overlap by one FIR output; the neighbour's first output comes through LDS.
+    xs[t] = acc[0];
+    __syncthreads();
+    const float2 nxt = (t + 1 < WG) ? xs[t + 1] : acc[R - 1];
+    float* out = reinterpret_cast<float*>(p.out);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const float2 y1 = (r + 1 < R) ? acc[r + 1] : nxt;
+      const uint32_t ml = local0 + r;
+      const uint64_t m = out0 + ml;
+      if (ml < (uint32_t)(WG * R - 1) && m < p.N) out[m] = fm_disc(acc[r], y1, p.fm_gain);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Kernel 1: polyphase-granule kernel, D a multiple of the granule width G.
+//   JC = tap rows per chunk (a multiple of R); a chunk covers JC*D taps.
+// ------------------------------------------------------------------------------------------------
+template <class TapT, class InT, int D, int R, int JC, int WG, bool VEC, int MODE>
+__global__ __launch_bounds__(WG) void k_fir_poly(FirParams p) {
+  using Geo = TileGeo<InT, D, R, WG>;
+  using OutT = typename Product<TapT, InT>::type;
+  constexpr int G = Geo::G;
+  constexpr int CPR = D / G;  // granule columns per input row
+  static_assert(D % G == 0, "polyphase kernel needs whole granules per row");
+  static_assert(JC % R == 0, "chunk rows must be whole thread segments");
+  constexpr int NWIN = R + JC - 1;
+
+  extern __shared__ __attribute__((aligned(16))) float4 lds[];
+  const InT* __restrict__ in = reinterpret_cast<const InT*>(p.in);
+  const TapBuf taps = make_tapbuf(p.taps, p.T * (uint32_t)sizeof(TapT));
+
+  const uint64_t out0 = (uint64_t)blockIdx.x * p.tile_stride;
+  const uint64_t S0 = out0 * D;
+  const uint32_t span = p.nch * JC * D;
+  const uint32_t NG = ((Geo::KT - 1) * D + span + G - 1) / G;
+
+  stage_tile<InT, Geo, WG, VEC, MODE>(lds, in, S0, NG, p);
+  __syncthreads();
+
+  OutT acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) set_zero(acc[r]);
+
+  const uint32_t t = threadIdx.x;
+  for (uint32_t c = 0; c < p.nch; ++c) {
+    const float4* __restrict__ seg = lds + (t + c * (JC / R)) * Geo::SGP;
+#pragma unroll
+    for (int h = 0; h < CPR; ++h) {
+      float4 win[NWIN];
+#pragma unroll
+      for (int u = 0; u < NWIN; ++u) {
+        const int q = u * CPR + h;
+        win[u] = seg[q + Geo::PAD * (q / Geo::SG)];
+      }
+      const uint32_t tap0 = c * JC * D + h * G;
+#pragma unroll
+      for (int j = 0; j < JC; ++j) {
+#pragma unroll
+        for (int e = 0; e < G; ++e) {
+          const TapT tv = tap_at<TapT>(taps, tap0 + j * D + e);
+#pragma unroll
+          for (int r = 0; r < R; ++r) mac(acc[r], granule_sample<InT>(win[r + j], e), tv);
+        }
+      }
+    }
+  }
+
+  float2* xs = reinterpret_cast<float2*>(lds + Geo::padded(NG - 1) + 1);
+  tile_epilogue<MODE, OutT, R, WG>(p, out0, acc, xs);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Kernel 2: contiguous-window kernel for small D (D = 1 in particular).
+//   IC = taps per chunk (a multiple of R*D).
+// ------------------------------------------------------------------------------------------------
+template <class TapT, class InT, int D, int R, int IC, int WG, bool VEC, int MODE>
+__global__ __launch_bounds__(WG) void k_fir_contig(FirParams p) {
+  using Geo = TileGeo<InT, D, R, WG>;
+  using OutT = typename Product<TapT, InT>::type;
+  constexpr int G = Geo::G;
+  static_assert(IC % (R * D) == 0, "chunk taps must be whole thread segments");
+  constexpr int W = (R - 1) * D + IC;  // window samples
+  constexpr int NWIN = (W + G - 1) / G;
+
+  extern __shared__ __attribute__((aligned(16))) float4 lds[];
+  const InT* __restrict__ in = reinterpret_cast<const InT*>(p.in);
+  const TapBuf taps = make_tapbuf(p.taps, p.T * (uint32_t)sizeof(TapT));
+
+  const uint64_t out0 = (uint64_t)blockIdx.x * p.tile_stride;
+  const uint64_t S0 = out0 * D;
+  const uint32_t span = p.nch * IC;
+  const uint32_t NG = ((Geo::KT - 1) * D + span + G - 1) / G;
+
+  stage_tile<InT, Geo, WG, VEC, MODE>(lds, in, S0, NG, p);
+  __syncthreads();
+
+  OutT acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) set_zero(acc[r]);
+
+  const uint32_t t = threadIdx.x;
+  for (uint32_t c = 0; c < p.nch; ++c) {
+    const float4* __restrict__ seg = lds + (t + c * (IC / (R * D))) * Geo::SGP;
+    float4 win[NWIN];
+#pragma unroll
+    for (int q = 0; q < NWIN; ++q) win[q] = seg[q + Geo::PAD * (q / Geo::SG)];
+#pragma unroll
+    for (int i = 0; i < IC; ++i) {
+      const TapT tv = tap_at<TapT>(taps, c * IC + i);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int s = r * D + i;
+        mac(acc[r], granule_sample<InT>(win[s / G], s % G), tv);
+      }
+    }
+  }
+
+  float2* xs = reinterpret_cast<float2*>(lds + Geo::padded(NG - 1) + 1);
+  tile_epilogue<MODE, OutT, R, WG>(p, out0, acc, xs);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Kernel 3: generic fallback (any D, any T, any alignment): one output per thread straight from
+// global memory (L1/L2 absorb the overlap). Used only where the tiled kernels do not apply.
+// In FM mode each thread also computes the next FIR output.
+// ------------------------------------------------------------------------------------------------
+template <class TapT, class InT, int MODE>
+__device__ __forceinline__ typename Product<TapT, InT>::type fir_point(const FirParams& p, uint64_t k) {
+  using OutT = typename Product<TapT, InT>::type;
+  const InT* __restrict__ in = reinterpret_cast<const InT*>(p.in);
+  const TapT* __restrict__ taps = reinterpret_cast<const TapT*>(p.taps);
+  OutT acc;
+  set_zero(acc);
+  const uint64_t s0 = k * p.D;
+  for (uint32_t i = 0; i < p.T; ++i) {
+    InT x = in[s0 + i];
+    if constexpr (MODE != kModeFir) {
+      x = nco_mix(x, (p.nco_n0 + (uint32_t)(s0 + i)) * p.nco_inc);
+    }
+    mac(acc, x, taps[i]);
+  }
+  return acc;
+}
+
+template <class TapT, class InT, int MODE>
+__global__ __launch_bounds__(256) void k_fir_generic(FirParams p) {
+  using OutT = typename Product<TapT, InT>::type;
+  const uint64_t k = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (k >= p.N) return;
+  if constexpr (MODE == kModeFir) {
+    reinterpret_cast<OutT*>(p.out)[k] = fir_point<TapT, InT, MODE>(p, k);
+  } else if constexpr (MODE == kModeAm) {
+    reinterpret_cast<float*>(p.out)[k] = am_env(fir_point<TapT, InT, MODE>(p, k));
+  } else {
+    const float2 y0 = fir_point<TapT, InT, MODE>(p, k);
+    const float2 y1 = fir_point<TapT, InT, MODE>(p, k + 1);
+    reinterpret_cast<float*>(p.out)[k] = fm_disc(y0, y1, p.fm_gain);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Host-side sizing helpers
+// ------------------------------------------------------------------------------------------------
+template <class InT, int D, int R, int WG>
+inline size_t poly_lds_bytes(uint32_t span_samples, int mode) {
+  using Geo = TileGeo<InT, D, R, WG>;
+  const uint32_t NG = ((Geo::KT - 1) * D + span_samples + Geo::G - 1) / Geo::G;
+  size_t bytes = (size_t)(Geo::padded(NG - 1) + 1) * 16u;
+  if (mode == kModeFm) bytes += (size_t)WG * sizeof(float2);
+  return bytes;
+}
+
+}  // namespace gsdr

@@ -1,0 +1,95 @@
+// gsdr-mi355x: fused NCO + low-pass FIR + decimation + FM discriminator / AM envelope.
+//   gsdrFmDemod  replaces reference src/fm.cu:181-218 (kernel k_Fm, fm.cu:21-69)
+//   gsdrAmDemod  replaces reference src/am.cu:52-81  (kernel k_Am, am.cu:21-50)
+// Both run the FIR engine of fir_engine.hpp with the NCO applied once per staged input sample
+// (the reference recomputes it per tap, adjustFrequency.cu:36-55) and the demodulator fused into the
+// epilogue, so the mixed and filtered intermediates never touch HBM.
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "fir_dispatch.hpp"
+#include "gsdr/am.h"
+#include "gsdr/fm.h"
+#include "gsdr/gsdr_ext.h"
+#include "launch.hpp"
+
+namespace gsdr {
+
+static constexpr float kPiF = 3.14159265358979323846f;
+
+// inc = llround(df / fs * 2^32) mod 2^32, df = tuning - channel (fm.cu:204, am.cu:68).
+static bool nco_increment(float fs, float tune, float chan, uint32_t* inc) {
+  if (!(fs > 0.0f) || !isfinite(fs)) return false;
+  const float df = tune - chan;
+  if (!isfinite(df)) return false;
+  const double turns = (double)df / (double)fs;
+  const double scaled = turns * 4294967296.0;
+  // reduce to [-2^32, 2^32] before rounding so llround never overflows
+  const double reduced = fmod(scaled, 4294967296.0);
+  *inc = (uint32_t)(int64_t)llround(reduced);
+  return true;
+}
+
+static hipError_t chain_entry(int mode, float fs, float tune, float chan, float dev, uint32_t decimation,
+                              size_t firstSampleIndex, const float* taps, size_t tapCount,
+                              const hipFloatComplex* input, float* output, size_t numOutputs, int32_t device,
+                              hipStream_t stream) {
+  if (numOutputs == 0) return hipSuccess;
+  if (decimation == 0 || output == nullptr || input == nullptr) return hipErrorInvalidValue;
+  if (tapCount > 0 && taps == nullptr) return hipErrorInvalidValue;
+  FirJob job;
+  if (!nco_increment(fs, tune, chan, &job.nco_inc)) return hipErrorInvalidValue;
+  job.in = input;
+  job.taps = taps;
+  job.out = output;
+  job.D = decimation;
+  job.T = tapCount;
+  job.N = numOutputs;
+  job.mode = mode;
+  job.nco_n0 = (uint32_t)firstSampleIndex;
+  if (mode == kModeFm) {
+    job.L = numOutputs * (size_t)decimation + tapCount;  // N + 1 FIR outputs
+    job.fm_gain = fs / (2.0f * kPiF * dev);              // as reference src/fm.cu:203
+  } else {
+    job.L = (numOutputs - 1) * (size_t)decimation + tapCount;
+  }
+  DeviceScope scope(device);
+  if (scope.status() != hipSuccess) return scope.status();
+  if (tapCount == 0) {
+    // y == 0 everywhere: the generic kernel evaluates the epilogue on zero without touching taps
+    return mode == kModeFm ? launch_generic<float, float2, kModeFm>(job, stream)
+                           : launch_generic<float, float2, kModeAm>(job, stream);
+  }
+  return mode == kModeFm ? launch_fir<float, float2, kModeFm>(job, stream)
+                         : launch_fir<float, float2, kModeAm>(job, stream);
+}
+
+}  // namespace gsdr
+
+GSDR_C_LINKAGE hipError_t gsdrFmDemod(float rfSampleRate, float tuningFrequency, float channelFrequency,
+                                      float frequencyDeviation, uint32_t decimation, size_t firstSampleIndex,
+                                      const float* lowPassTaps, size_t numLowPassTaps, const hipFloatComplex* input,
+                                      float* output, size_t numOutputs, int32_t cudaDevice,
+                                      hipStream_t cudaStream) GSDR_NO_EXCEPT {
+  return gsdr::chain_entry(gsdr::kModeFm, rfSampleRate, tuningFrequency, channelFrequency, frequencyDeviation,
+                           decimation, firstSampleIndex, lowPassTaps, numLowPassTaps, input, output, numOutputs,
+                           cudaDevice, cudaStream);
+}
+
+GSDR_C_LINKAGE hipError_t gsdrAmDemod(float rfSampleRate, float tuningFrequency, float channelFrequency,
+                                      uint32_t decimation, size_t firstSampleIndex, const float* lowPassTaps,
+                                      size_t numLowPassTaps, const hipFloatComplex* input, float* output,
+                                      size_t numElements, int32_t cudaDevice, hipStream_t cudaStream) GSDR_NO_EXCEPT {
+  return gsdr::chain_entry(gsdr::kModeAm, rfSampleRate, tuningFrequency, channelFrequency, 1.0f, decimation,
+                           firstSampleIndex, lowPassTaps, numLowPassTaps, input, output, numElements, cudaDevice,
+                           cudaStream);
+}
+
+GSDR_C_LINKAGE uint32_t gsdrNcoPhaseIncrement(float rfSampleRate, float tuningFrequency,
+                                              float channelFrequency) GSDR_NO_EXCEPT {
+  uint32_t inc = 0;
+  (void)gsdr::nco_increment(rfSampleRate, tuningFrequency, channelFrequency, &inc);
+  return inc;
+}
+
+GSDR_C_LINKAGE const char* gsdrVersion(void) GSDR_NO_EXCEPT { return "gsdr-mi355x 0.1.0 (gfx950)"; }

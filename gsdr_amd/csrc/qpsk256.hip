@@ -1,0 +1,280 @@
+// gsdr-mi355x: 256-point constellation modulate / demodulate.
+// Replaces reference src/qpsk256.cu (tables :25-71, modulate :74-151, demodulate :154-259,
+// wrappers :262-431; header qpsk256.h:125-230).
+//
+// Tables are built on the host, in float, with exactly the reference's expressions
+// (qpsk256.cu:33-34, 54-56, 64-67), and uploaded per device on the caller's stream. Each workgroup
+// copies the 2 KiB table it needs into LDS, so lookups are LDS reads rather than divergent
+// constant-cache accesses.
+//
+// Demodulation decision (bit-exact contract shared with the CPU oracle): the first index attaining
+// the minimum of d_i = fl(fl(dx*dx) + fl(dy*dy)) over all 256 points, strict '<', d initialised to
+// +inf (so a NaN/inf symbol maps to 0), as the reference's exhaustive argmin (qpsk256.cu:171-181) with
+// the squared distance in place of cuCabsf. For the rectangular grid a received point inside
+// |re|,|im| <= 4|a| can only be won by one of the 3 x 3 grid points around its per-axis nearest level
+// (every other point is farther by >= 0.035 a^2, far beyond float rounding), so those 9 candidates are
+// evaluated in ascending index order with the identical expression; anything else takes the
+// exhaustive path. Circular tables always take the exhaustive path.
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "gsdr/qpsk256.h"
+#include "launch.hpp"
+
+namespace gsdr {
+
+constexpr int kCBlock = 256;
+constexpr int kCSym = 16;  // symbols per thread
+
+// [0] rectangular, [1] circular; per device (module globals are per-device copies).
+__constant__ float2 c_qpsk256_tables[2][256];
+
+struct C256Streams {
+  const void* in[4];
+  void* out[4];
+};
+
+__device__ __forceinline__ float sqdist(float2 r, float2 c) {
+  const float dx = __fsub_rn(r.x, c.x);
+  const float dy = __fsub_rn(r.y, c.y);
+  return __fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy));
+}
+
+__device__ __forceinline__ uint32_t demod_exhaustive(const float2* __restrict__ tab, float2 r) {
+  float best = INFINITY;
+  uint32_t idx = 0;
+  for (uint32_t i = 0; i < 256; ++i) {
+    const float d = sqdist(r, tab[i]);
+    if (d < best) {
+      best = d;
+      idx = i;
+    }
+  }
+  return idx;
+}
+
+__device__ __forceinline__ int nearest_level(float v, float scale) {
+  // level i sits at (i - 7.5) / 7.5 * a  =>  i ~= v * (7.5 / a) + 7.5
+  const float u = fmaf(v, scale, 7.5f);
+  int i = (int)rintf(u);
+  return i < 0 ? 0 : (i > 15 ? 15 : i);
+}
+
+__device__ __forceinline__ uint32_t demod_rect(const float2* __restrict__ tab, float2 r, float a, float scale) {
+  const float lim = 4.0f * fabsf(a);
+  if (!(fabsf(r.x) <= lim && fabsf(r.y) <= lim) || !(scale == scale) || isinf(scale)) {
+    return demod_exhaustive(tab, r);
+  }
+  const int i0 = nearest_level(r.x, scale);
+  const int q0 = nearest_level(r.y, scale);
+  float best = INFINITY;
+  uint32_t idx = 0;
+#pragma unroll
+  for (int di = -1; di <= 1; ++di) {
+    const int i = i0 + di;
+    if (i < 0 || i > 15) continue;
+#pragma unroll
+    for (int dq = -1; dq <= 1; ++dq) {
+      const int q = q0 + dq;
+      if (q < 0 || q > 15) continue;
+      const uint32_t k = (uint32_t)(i * 16 + q);
+      const float d = sqdist(r, tab[k]);
+      if (d < best) {
+        best = d;
+        idx = k;
+      }
+    }
+  }
+  return idx;
+}
+
+__device__ __forceinline__ void load_table(float2* lds_tab, uint32_t type) {
+  const float2* src = c_qpsk256_tables[type == 0 ? 0 : 1];
+  for (uint32_t i = threadIdx.x; i < 256; i += kCBlock) lds_tab[i] = src[i];
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kCBlock) void k_c256_mod(C256Streams st, uint32_t n, uint32_t type) {
+  __shared__ float2 tab[256];
+  load_table(tab, type);
+  const uint8_t* __restrict__ in = reinterpret_cast<const uint8_t*>(st.in[blockIdx.y]);
+  float2* __restrict__ out = reinterpret_cast<float2*>(st.out[blockIdx.y]);
+  const uint64_t s0 = ((uint64_t)blockIdx.x * kCBlock + threadIdx.x) * kCSym;
+  if (s0 >= n) return;
+  if (s0 + kCSym <= n && (reinterpret_cast<uintptr_t>(in + s0) & 15u) == 0 &&
+      (reinterpret_cast<uintptr_t>(out + s0) & 15u) == 0) {
+    const uint4 w = *reinterpret_cast<const uint4*>(in + s0);
+    const uint32_t words[4] = {w.x, w.y, w.z, w.w};
+    float4* o = reinterpret_cast<float4*>(out + s0);
+#pragma unroll
+    for (int q = 0; q < kCSym / 2; ++q) {
+      const uint32_t word = words[q / 2];
+      const float2 p0 = tab[(word >> (16 * (q & 1))) & 0xffu];
+      const float2 p1 = tab[(word >> (16 * (q & 1) + 8)) & 0xffu];
+      o[q] = make_float4(p0.x, p0.y, p1.x, p1.y);
+    }
+  } else {
+    for (int k = 0; k < kCSym; ++k) {
+      if (s0 + k < n) out[s0 + k] = tab[in[s0 + k]];
+    }
+  }
+}
+
+__global__ __launch_bounds__(kCBlock) void k_c256_demod(C256Streams st, uint32_t n, uint32_t type) {
+  __shared__ float2 tab[256];
+  load_table(tab, type);
+  const float2* __restrict__ in = reinterpret_cast<const float2*>(st.in[blockIdx.y]);
+  uint8_t* __restrict__ out = reinterpret_cast<uint8_t*>(st.out[blockIdx.y]);
+  const uint64_t s0 = ((uint64_t)blockIdx.x * kCBlock + threadIdx.x) * kCSym;
+  if (s0 >= n) return;
+  const float a = tab[255].x;  // rectangular: (15 - 7.5) / 7.5 * a == a exactly
+  const float scale = 7.5f / a;
+  const bool rect = (type == 0);
+  if (s0 + kCSym <= n && (reinterpret_cast<uintptr_t>(in + s0) & 15u) == 0 &&
+      (reinterpret_cast<uintptr_t>(out + s0) & 15u) == 0) {
+    const float4* src = reinterpret_cast<const float4*>(in + s0);
+    uint32_t words[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int q = 0; q < kCSym / 2; ++q) {
+      const float4 v = src[q];
+      const float2 r0 = make_float2(v.x, v.y);
+      const float2 r1 = make_float2(v.z, v.w);
+      const uint32_t i0 = rect ? demod_rect(tab, r0, a, scale) : demod_exhaustive(tab, r0);
+      const uint32_t i1 = rect ? demod_rect(tab, r1, a, scale) : demod_exhaustive(tab, r1);
+      words[q / 2] |= (i0 | (i1 << 8)) << (16 * (q & 1));
+    }
+    *reinterpret_cast<uint4*>(out + s0) = make_uint4(words[0], words[1], words[2], words[3]);
+  } else {
+    for (int k = 0; k < kCSym; ++k) {
+      if (s0 + k < n) {
+        const float2 r = in[s0 + k];
+        out[s0 + k] = (uint8_t)(rect ? demod_rect(tab, r, a, scale) : demod_exhaustive(tab, r));
+      }
+    }
+  }
+}
+
+static hipError_t c256_launch(bool modulate, const C256Streams& st, int nstreams, uint32_t n, uint32_t type,
+                              int32_t device, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  for (int s = 0; s < nstreams; ++s) {
+    if (st.in[s] == nullptr || st.out[s] == nullptr) return hipErrorInvalidValue;
+  }
+  DeviceScope scope(device);
+  if (scope.status() != hipSuccess) return scope.status();
+  const uint32_t blocks = ceil_div<uint32_t>(ceil_div<uint32_t>(n, kCSym), kCBlock);
+  const dim3 grid(blocks, (uint32_t)nstreams);
+  if (modulate) {
+    k_c256_mod<<<grid, dim3(kCBlock), 0, stream>>>(st, n, type);
+  } else {
+    k_c256_demod<<<grid, dim3(kCBlock), 0, stream>>>(st, n, type);
+  }
+  return launch_status();
+}
+
+static constexpr float kPiF = 3.14159265358979323846f;
+
+// Host construction, float arithmetic in the reference's evaluation order.
+static void build_table(uint32_t type, float amplitude, float2* t) {
+  if (type == 0) {
+    for (int i = 0; i < 16; ++i) {
+      for (int q = 0; q < 16; ++q) {
+        const float I = ((float)i - 7.5f) / 7.5f * amplitude;
+        const float Q = ((float)q - 7.5f) / 7.5f * amplitude;
+        t[i * 16 + q] = make_float2(I, Q);
+      }
+    }
+    return;
+  }
+  static const int kPoints[8] = {1, 8, 16, 24, 32, 40, 48, 56};
+  static const float kRadii[8] = {0.0f, 0.3f, 0.6f, 0.85f, 1.1f, 1.35f, 1.6f, 1.85f};
+  int idx = 0;
+  for (int c = 0; c < 8 && idx < 256; ++c) {
+    const int points = kPoints[c] < 256 - idx ? kPoints[c] : 256 - idx;
+    const float radius = kRadii[c] * amplitude;
+    for (int p = 0; p < points && idx < 256; ++p) {
+      const float angle = 2.0f * kPiF * (float)p / (float)points + ((float)c * 0.5f);
+      t[idx++] = make_float2(radius * cosf(angle), radius * sinf(angle));
+    }
+  }
+  while (idx < 256) {
+    const float angle = 2.0f * kPiF * (float)idx / 256.0f;
+    const float radius = amplitude * 0.95f;
+    t[idx] = make_float2(radius * cosf(angle), radius * sinf(angle));
+    ++idx;
+  }
+}
+
+}  // namespace gsdr
+
+using gsdr::C256Streams;
+
+GSDR_C_LINKAGE hipError_t gsdrQpsk256InitConstellation(uint32_t constellationType, float amplitude,
+                                                       int32_t cudaDevice, hipStream_t cudaStream) GSDR_NO_EXCEPT {
+  gsdr::DeviceScope scope(cudaDevice);
+  if (scope.status() != hipSuccess) return scope.status();
+  float2 table[256];
+  gsdr::build_table(constellationType, amplitude, table);
+  const size_t offset = (constellationType == 0 ? 0 : 1) * sizeof(table);
+  hipError_t st = hipMemcpyToSymbolAsync(HIP_SYMBOL(gsdr::c_qpsk256_tables), table, sizeof(table), offset,
+                                         hipMemcpyHostToDevice, cudaStream);
+  if (st != hipSuccess) return st;
+  // the host table lives on this stack frame: wait for the copy before returning
+  return hipStreamSynchronize(cudaStream);
+}
+
+GSDR_C_LINKAGE hipError_t gsdrQpsk256Modulate(const uint8_t* inputBytes, hipFloatComplex* output, uint32_t numSymbols,
+                                              float amplitude, uint32_t constellationType, int32_t cudaDevice,
+                                              hipStream_t cudaStream) GSDR_NO_EXCEPT {
+  (void)amplitude;  // scale is fixed by InitConstellation, as in the reference (qpsk256.cu:74-101)
+  C256Streams st{};
+  st.in[0] = inputBytes;
+  st.out[0] = output;
+  return gsdr::c256_launch(true, st, 1, numSymbols, constellationType, cudaDevice, cudaStream);
+}
+
+GSDR_C_LINKAGE hipError_t gsdrQpsk256Demodulate(const hipFloatComplex* input, uint8_t* outputBytes,
+                                                uint32_t numSymbols, uint32_t constellationType, int32_t cudaDevice,
+                                                hipStream_t cudaStream) GSDR_NO_EXCEPT {
+  C256Streams st{};
+  st.in[0] = input;
+  st.out[0] = outputBytes;
+  return gsdr::c256_launch(false, st, 1, numSymbols, constellationType, cudaDevice, cudaStream);
+}
+
+GSDR_C_LINKAGE hipError_t gsdrQpsk256Modulate4x(const uint8_t* inputBytes0, const uint8_t* inputBytes1,
+                                                const uint8_t* inputBytes2, const uint8_t* inputBytes3,
+                                                hipFloatComplex* output0, hipFloatComplex* output1,
+                                                hipFloatComplex* output2, hipFloatComplex* output3,
+                                                uint32_t numSymbols, float amplitude, uint32_t constellationType,
+                                                int32_t cudaDevice, hipStream_t cudaStream) GSDR_NO_EXCEPT {
+  (void)amplitude;
+  C256Streams st{};
+  st.in[0] = inputBytes0;
+  st.in[1] = inputBytes1;
+  st.in[2] = inputBytes2;
+  st.in[3] = inputBytes3;
+  st.out[0] = output0;
+  st.out[1] = output1;
+  st.out[2] = output2;
+  st.out[3] = output3;
+  return gsdr::c256_launch(true, st, 4, numSymbols, constellationType, cudaDevice, cudaStream);
+}
+
+GSDR_C_LINKAGE hipError_t gsdrQpsk256Demodulate4x(const hipFloatComplex* input0, const hipFloatComplex* input1,
+                                                  const hipFloatComplex* input2, const hipFloatComplex* input3,
+                                                  uint8_t* outputBytes0, uint8_t* outputBytes1, uint8_t* outputBytes2,
+                                                  uint8_t* outputBytes3, uint32_t numSymbols,
+                                                  uint32_t constellationType, int32_t cudaDevice,
+                                                  hipStream_t cudaStream) GSDR_NO_EXCEPT {
+  C256Streams st{};
+  st.in[0] = input0;
+  st.in[1] = input1;
+  st.in[2] = input2;
+  st.in[3] = input3;
+  st.out[0] = outputBytes0;
+  st.out[1] = outputBytes1;
+  st.out[2] = outputBytes2;
+  st.out[3] = outputBytes3;
+  return gsdr::c256_launch(false, st, 4, numSymbols, constellationType, cudaDevice, cudaStream);
+}

@@ -1,0 +1,237 @@
+"""torch-tensor conveniences over the C ABI (gsdr_amd.abi).
+
+Each function checks shapes/dtypes, allocates the output if none is given, and calls the matching
+`gsdr*` entry point on the tensor's device and on torch's current stream for that device, raising
+GsdrError on a non-zero hipError_t. Complex tensors are torch.complex64 (interleaved float pairs,
+the hipFloatComplex layout).
+"""
+from __future__ import annotations
+
+import torch
+
+from .abi import check, lib
+
+__all__ = [
+    "fir", "fir_variant", "fm_demod", "am_demod", "quad_fm_demod", "quad_am_demod", "magnitude",
+    "qpsk_modulate", "qpsk_demodulate", "qpsk_modulate_4x", "qpsk_demodulate_4x",
+    "qpsk_modulate_templated", "qpsk_demodulate_templated",
+    "qpsk256_init", "qpsk256_modulate", "qpsk256_demodulate", "qpsk256_modulate_4x", "qpsk256_demodulate_4x",
+    "nco_phase_increment", "stream_of",
+]
+
+
+def stream_of(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _dev(t: torch.Tensor) -> int:
+    if t.device.type != "cuda":
+        raise ValueError("gsdr_amd operates on device tensors (got %s)" % t.device)
+    return t.device.index
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def _require(t: torch.Tensor, dtype, name: str, min_len: int = 0):
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if t.numel() < min_len:
+        raise ValueError(f"{name}: need at least {min_len} elements, got {t.numel()}")
+
+
+_FIR = {
+    (torch.float32, torch.complex64): ("gsdrFirFC", torch.complex64),
+    (torch.float32, torch.float32): ("gsdrFirFF", torch.float32),
+    (torch.complex64, torch.complex64): ("gsdrFirCC", torch.complex64),
+    (torch.complex64, torch.float32): ("gsdrFirCF", torch.complex64),
+}
+
+
+def _fir_prepare(taps, x, decimation, num_outputs, out):
+    key = (taps.dtype, x.dtype)
+    if key not in _FIR:
+        raise TypeError(f"unsupported tap/input dtypes {key}")
+    name, odt = _FIR[key]
+    T = taps.numel()
+    if num_outputs is None:
+        num_outputs = (x.numel() - T) // decimation + 1 if x.numel() >= T else 0
+    if num_outputs > 0:
+        _require(x, x.dtype, "input", (num_outputs - 1) * decimation + T)
+    if out is None:
+        out = torch.empty(num_outputs, dtype=odt, device=x.device)
+    _require(out, odt, "output", num_outputs)
+    return name, num_outputs, out
+
+
+def fir(taps: torch.Tensor, x: torch.Tensor, decimation: int = 1, num_outputs: int | None = None,
+        out: torch.Tensor | None = None) -> torch.Tensor:
+    """y[k] = sum_i x[k*decimation + i] * taps[i] (gsdrFirFC/FF/CC/CF by dtype)."""
+    name, n, out = _fir_prepare(taps, x, decimation, num_outputs, out)
+    check(name, getattr(lib, name)(decimation, _ptr(taps), taps.numel(), _ptr(x), _ptr(out), n, _dev(x),
+                                   stream_of(x)))
+    return out
+
+
+def fir_variant(variant: int, taps: torch.Tensor, x: torch.Tensor, decimation: int = 4,
+                num_outputs: int | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+    """gsdrFirFC with an explicit tile shape (tuning; see gsdr_ext.h)."""
+    name, n, out = _fir_prepare(taps, x, decimation, num_outputs, out)
+    if name != "gsdrFirFC":
+        raise TypeError("fir_variant is FC only")
+    check("gsdrxFirFCVariant", lib.gsdrxFirFCVariant(variant, decimation, _ptr(taps), taps.numel(), _ptr(x),
+                                                     _ptr(out), n, _dev(x), stream_of(x)))
+    return out
+
+
+def fm_demod(x, taps, rf_sample_rate, tuning_frequency, channel_frequency, frequency_deviation, decimation,
+             first_sample_index=0, num_outputs=None, out=None):
+    """gsdrFmDemod: NCO shift + low-pass FIR + decimation + FM discriminator (fm.h)."""
+    _require(x, torch.complex64, "input")
+    _require(taps, torch.float32, "taps")
+    T = taps.numel()
+    if num_outputs is None:
+        num_outputs = max(0, (x.numel() - T) // decimation)
+    if num_outputs > 0:
+        _require(x, torch.complex64, "input", num_outputs * decimation + T)
+    if out is None:
+        out = torch.empty(num_outputs, dtype=torch.float32, device=x.device)
+    _require(out, torch.float32, "output", num_outputs)
+    check("gsdrFmDemod", lib.gsdrFmDemod(rf_sample_rate, tuning_frequency, channel_frequency, frequency_deviation,
+                                         decimation, first_sample_index, _ptr(taps), T, _ptr(x), _ptr(out),
+                                         num_outputs, _dev(x), stream_of(x)))
+    return out
+
+
+def am_demod(x, taps, rf_sample_rate, tuning_frequency, channel_frequency, decimation, first_sample_index=0,
+             num_outputs=None, out=None):
+    """gsdrAmDemod: NCO shift + low-pass FIR + decimation + envelope (am.h)."""
+    _require(x, torch.complex64, "input")
+    _require(taps, torch.float32, "taps")
+    T = taps.numel()
+    if num_outputs is None:
+        num_outputs = (x.numel() - T) // decimation + 1 if x.numel() >= T else 0
+    if num_outputs > 0:
+        _require(x, torch.complex64, "input", (num_outputs - 1) * decimation + T)
+    if out is None:
+        out = torch.empty(num_outputs, dtype=torch.float32, device=x.device)
+    _require(out, torch.float32, "output", num_outputs)
+    check("gsdrAmDemod", lib.gsdrAmDemod(rf_sample_rate, tuning_frequency, channel_frequency, decimation,
+                                         first_sample_index, _ptr(taps), T, _ptr(x), _ptr(out), num_outputs,
+                                         _dev(x), stream_of(x)))
+    return out
+
+
+def quad_fm_demod(x, gain, num_outputs=None, out=None):
+    _require(x, torch.complex64, "input")
+    n = max(0, x.numel() - 1) if num_outputs is None else num_outputs
+    if n > 0:
+        _require(x, torch.complex64, "input", n + 1)
+    out = torch.empty(n, dtype=torch.float32, device=x.device) if out is None else out
+    _require(out, torch.float32, "output", n)
+    check("gsdrQuadFmDemod", lib.gsdrQuadFmDemod(_ptr(x), _ptr(out), gain, n, _dev(x), stream_of(x)))
+    return out
+
+
+def quad_am_demod(x, num_outputs=None, out=None):
+    _require(x, torch.complex64, "input")
+    n = x.numel() if num_outputs is None else num_outputs
+    _require(x, torch.complex64, "input", n)
+    out = torch.empty(n, dtype=torch.float32, device=x.device) if out is None else out
+    _require(out, torch.float32, "output", n)
+    check("gsdrQuadAmDemod", lib.gsdrQuadAmDemod(_ptr(x), _ptr(out), n, _dev(x), stream_of(x)))
+    return out
+
+
+def magnitude(x, out=None):
+    _require(x, torch.complex64, "input")
+    n = x.numel()
+    out = torch.empty(n, dtype=torch.float32, device=x.device) if out is None else out
+    _require(out, torch.float32, "output", n)
+    check("gsdrMagnitude", lib.gsdrMagnitude(_ptr(x), _ptr(out), n, _dev(x), stream_of(x)))
+    return out
+
+
+def qpsk_modulate(bits, num_symbols, amplitude=1.0, out=None):
+    _require(bits, torch.uint8, "inputBits", (num_symbols + 3) // 4)
+    out = torch.empty(num_symbols, dtype=torch.complex64, device=bits.device) if out is None else out
+    _require(out, torch.complex64, "output", num_symbols)
+    check("gsdrQpskModulate", lib.gsdrQpskModulate(_ptr(bits), _ptr(out), num_symbols, amplitude, _dev(bits),
+                                                   stream_of(bits)))
+    return out
+
+
+def qpsk_demodulate(x, num_symbols=None, out=None):
+    _require(x, torch.complex64, "input")
+    n = x.numel() if num_symbols is None else num_symbols
+    out = torch.zeros((n + 3) // 4, dtype=torch.uint8, device=x.device) if out is None else out
+    _require(out, torch.uint8, "outputBits", (n + 3) // 4)
+    check("gsdrQpskDemodulate", lib.gsdrQpskDemodulate(_ptr(x), _ptr(out), n, _dev(x), stream_of(x)))
+    return out
+
+
+def qpsk_modulate_4x(bits4, outs4, num_symbols, amplitude=1.0):
+    check("gsdrQpskModulate4x", lib.gsdrQpskModulate4x(*[_ptr(b) for b in bits4], *[_ptr(o) for o in outs4],
+                                                       num_symbols, amplitude, _dev(outs4[0]),
+                                                       stream_of(outs4[0])))
+
+
+def qpsk_demodulate_4x(ins4, bits4, num_symbols):
+    check("gsdrQpskDemodulate4x", lib.gsdrQpskDemodulate4x(*[_ptr(i) for i in ins4], *[_ptr(b) for b in bits4],
+                                                           num_symbols, _dev(ins4[0]), stream_of(ins4[0])))
+
+
+def qpsk_modulate_templated(bits, out, num_symbols, amplitude, num_streams):
+    check("gsdrQpskModulateTemplated", lib.gsdrQpskModulateTemplated(_ptr(bits), _ptr(out), num_symbols, amplitude,
+                                                                     num_streams, _dev(out), stream_of(out)))
+
+
+def qpsk_demodulate_templated(x, bits, num_symbols, num_streams):
+    check("gsdrQpskDemodulateTemplated", lib.gsdrQpskDemodulateTemplated(_ptr(x), _ptr(bits), num_symbols,
+                                                                         num_streams, _dev(x), stream_of(x)))
+
+
+def qpsk256_init(constellation_type, amplitude, device=None):
+    dev = torch.cuda.current_device() if device is None else device
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    check("gsdrQpsk256InitConstellation", lib.gsdrQpsk256InitConstellation(constellation_type, amplitude, dev,
+                                                                           stream))
+
+
+def qpsk256_modulate(symbols, constellation_type, amplitude=1.0, out=None):
+    _require(symbols, torch.uint8, "inputBytes")
+    n = symbols.numel()
+    out = torch.empty(n, dtype=torch.complex64, device=symbols.device) if out is None else out
+    _require(out, torch.complex64, "output", n)
+    check("gsdrQpsk256Modulate", lib.gsdrQpsk256Modulate(_ptr(symbols), _ptr(out), n, amplitude, constellation_type,
+                                                         _dev(symbols), stream_of(symbols)))
+    return out
+
+
+def qpsk256_demodulate(x, constellation_type, out=None):
+    _require(x, torch.complex64, "input")
+    n = x.numel()
+    out = torch.empty(n, dtype=torch.uint8, device=x.device) if out is None else out
+    _require(out, torch.uint8, "outputBytes", n)
+    check("gsdrQpsk256Demodulate", lib.gsdrQpsk256Demodulate(_ptr(x), _ptr(out), n, constellation_type, _dev(x),
+                                                             stream_of(x)))
+    return out
+
+
+def qpsk256_modulate_4x(ins4, outs4, num_symbols, constellation_type, amplitude=1.0):
+    check("gsdrQpsk256Modulate4x", lib.gsdrQpsk256Modulate4x(*[_ptr(i) for i in ins4], *[_ptr(o) for o in outs4],
+                                                             num_symbols, amplitude, constellation_type,
+                                                             _dev(outs4[0]), stream_of(outs4[0])))
+
+
+def qpsk256_demodulate_4x(ins4, outs4, num_symbols, constellation_type):
+    check("gsdrQpsk256Demodulate4x", lib.gsdrQpsk256Demodulate4x(*[_ptr(i) for i in ins4], *[_ptr(o) for o in outs4],
+                                                                 num_symbols, constellation_type, _dev(ins4[0]),
+                                                                 stream_of(ins4[0])))
+
+
+def nco_phase_increment(rf_sample_rate, tuning_frequency, channel_frequency) -> int:
+    return int(lib.gsdrNcoPhaseIncrement(rf_sample_rate, tuning_frequency, channel_frequency))

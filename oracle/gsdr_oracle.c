@@ -1,0 +1,307 @@
+/*
+ * gsdr CPU oracle -- TEST INFRASTRUCTURE ONLY (see gsdr_oracle.h for the contract and pinning).
+ * Compiled with -ffp-contract=off: every fused multiply-add below is an explicit fmaf, every other
+ * product and sum is rounded separately, in the order written.
+ */
+#include "gsdr_oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+static const double kTwoPi = 6.283185307179586476925286766559;
+static const float kPiF = 3.14159265358979323846f;
+
+/* ---------------------------------------------------------------- A.1 FIR (fir.cu:26-71) */
+
+void oracle_fir_ff(size_t D, const float* t, size_t T, const float* x, float* y, size_t k0, size_t k1) {
+  for (size_t k = k0; k < k1; ++k) {
+    const float* xs = x + k * D;
+    float acc = 0.0f;
+    for (size_t i = 0; i < T; ++i) acc = fmaf(xs[i], t[i], acc);
+    y[k] = acc;
+  }
+}
+
+/* c * r: (c.re * r, c.im * r)  (cuComplexOperatorOverloads.cuh:29-31) */
+void oracle_fir_fc(size_t D, const float* t, size_t T, const float* x, float* y, size_t k0, size_t k1) {
+  for (size_t k = k0; k < k1; ++k) {
+    const float* xs = x + 2 * k * D;
+    float re = 0.0f, im = 0.0f;
+    for (size_t i = 0; i < T; ++i) {
+      re = fmaf(xs[2 * i], t[i], re);
+      im = fmaf(xs[2 * i + 1], t[i], im);
+    }
+    y[2 * k] = re;
+    y[2 * k + 1] = im;
+  }
+}
+
+/* cuCmulf(x, t) = (x.re t.re - x.im t.im, x.re t.im + x.im t.re) (cuh:25-27) */
+void oracle_fir_cc(size_t D, const float* t, size_t T, const float* x, float* y, size_t k0, size_t k1) {
+  for (size_t k = k0; k < k1; ++k) {
+    const float* xs = x + 2 * k * D;
+    float re = 0.0f, im = 0.0f;
+    for (size_t i = 0; i < T; ++i) {
+      const float xr = xs[2 * i], xi = xs[2 * i + 1], tr = t[2 * i], ti = t[2 * i + 1];
+      re = fmaf(xr, tr, re);
+      re = fmaf(-xi, ti, re);
+      im = fmaf(xr, ti, im);
+      im = fmaf(xi, tr, im);
+    }
+    y[2 * k] = re;
+    y[2 * k + 1] = im;
+  }
+}
+
+/* r * c with r = real input sample, c = complex tap (cuh:33) */
+void oracle_fir_cf(size_t D, const float* t, size_t T, const float* x, float* y, size_t k0, size_t k1) {
+  for (size_t k = k0; k < k1; ++k) {
+    const float* xs = x + k * D;
+    float re = 0.0f, im = 0.0f;
+    for (size_t i = 0; i < T; ++i) {
+      re = fmaf(t[2 * i], xs[i], re);
+      im = fmaf(t[2 * i + 1], xs[i], im);
+    }
+    y[2 * k] = re;
+    y[2 * k + 1] = im;
+  }
+}
+
+typedef struct {
+  size_t D, T, k0, k1;
+  const float* t;
+  const float* x;
+  float* y;
+} FcJob;
+
+static void* fc_worker(void* arg) {
+  const FcJob* j = (const FcJob*)arg;
+  oracle_fir_fc(j->D, j->t, j->T, j->x, j->y, j->k0, j->k1);
+  return NULL;
+}
+
+void oracle_fir_fc_mt(size_t D, const float* t, size_t T, const float* x, float* y, size_t N, int nthreads) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  pthread_t th[256];
+  FcJob jobs[256];
+  for (int w = 0; w < nthreads; ++w) {
+    jobs[w].D = D;
+    jobs[w].T = T;
+    jobs[w].t = t;
+    jobs[w].x = x;
+    jobs[w].y = y;
+    jobs[w].k0 = N * (size_t)w / (size_t)nthreads;
+    jobs[w].k1 = N * (size_t)(w + 1) / (size_t)nthreads;
+  }
+  for (int w = 1; w < nthreads; ++w) pthread_create(&th[w], NULL, fc_worker, &jobs[w]);
+  fc_worker(&jobs[0]);
+  for (int w = 1; w < nthreads; ++w) pthread_join(th[w], NULL);
+}
+
+void oracle_fir_bound_fc(size_t D, const float* t, size_t T, const float* x, float* s, size_t k0, size_t k1) {
+  for (size_t k = k0; k < k1; ++k) {
+    const float* xs = x + 2 * k * D;
+    double acc = 0.0;
+    for (size_t i = 0; i < T; ++i) acc += fabs((double)t[i]) * hypot((double)xs[2 * i], (double)xs[2 * i + 1]);
+    s[k] = (float)acc;
+  }
+}
+
+/* ---------------------------------------------------------------- A.3 NCO */
+
+uint32_t oracle_nco_inc(float fs, float tune, float chan) {
+  if (!(fs > 0.0f) || !isfinite(fs)) return 0;
+  const float df = tune - chan; /* float, as fm.cu:204 */
+  if (!isfinite(df)) return 0;
+  const double scaled = ((double)df / (double)fs) * 4294967296.0;
+  const double reduced = fmod(scaled, 4294967296.0);
+  return (uint32_t)(int64_t)llround(reduced);
+}
+
+static inline void nco_rot(float xr, float xi, uint32_t phase, float* zr, float* zi) {
+  const double th = kTwoPi * ((double)phase / 4294967296.0);
+  const float c = (float)cos(th), s = (float)sin(th);
+  /* x * (c + j s), cuCmulf order (adjustFrequency.cu:50-51) */
+  *zr = xr * c - xi * s;
+  *zi = xr * s + xi * c;
+}
+
+void oracle_nco_mix(const float* x, float* z, uint64_t n0, uint32_t inc, size_t i0, size_t i1) {
+  for (size_t n = i0; n < i1; ++n) {
+    const uint32_t p = (uint32_t)((uint32_t)(n0 + n) * inc);
+    nco_rot(x[2 * n], x[2 * n + 1], p, &z[2 * n], &z[2 * n + 1]);
+  }
+}
+
+/* ---------------------------------------------------------------- A.4 chains */
+
+static void chain_point(uint32_t inc, uint32_t D, uint64_t n0, const float* taps, size_t T, const float* x,
+                        size_t m, float* yr, float* yi) {
+  float re = 0.0f, im = 0.0f;
+  const size_t s0 = m * (size_t)D;
+  for (size_t i = 0; i < T; ++i) {
+    const size_t n = s0 + i;
+    float zr, zi;
+    nco_rot(x[2 * n], x[2 * n + 1], (uint32_t)((uint32_t)(n0 + n) * inc), &zr, &zi);
+    re = fmaf(zr, taps[i], re);
+    im = fmaf(zi, taps[i], im);
+  }
+  *yr = re;
+  *yi = im;
+}
+
+void oracle_chain_fir(float fs, float tune, float chan, uint32_t D, uint64_t n0, const float* taps, size_t T,
+                      const float* x, float* y, size_t m0, size_t m1) {
+  const uint32_t inc = oracle_nco_inc(fs, tune, chan);
+  for (size_t m = m0; m < m1; ++m) chain_point(inc, D, n0, taps, T, x, m, &y[2 * m], &y[2 * m + 1]);
+}
+
+/* g * atan2(Im, Re)(y1 * conj(y0)) (fm.cu:66-68, quad_demod.cu:30-31) */
+static inline float disc(float r0, float i0, float r1, float i1, float g) {
+  const float re = r1 * r0 + i1 * i0;
+  const float im = i1 * r0 - r1 * i0;
+  return g * atan2f(im, re);
+}
+
+void oracle_fm_demod(float fs, float tune, float chan, float dev, uint32_t D, uint64_t n0, const float* taps,
+                     size_t T, const float* x, float* out, size_t m0, size_t m1) {
+  if (m1 <= m0) return;
+  const uint32_t inc = oracle_nco_inc(fs, tune, chan);
+  const float g = fs / (2.0f * kPiF * dev); /* fm.cu:203 */
+  float pr, pi;
+  chain_point(inc, D, n0, taps, T, x, m0, &pr, &pi);
+  for (size_t m = m0; m < m1; ++m) {
+    float nr, ni;
+    chain_point(inc, D, n0, taps, T, x, m + 1, &nr, &ni);
+    out[m] = disc(pr, pi, nr, ni, g);
+    pr = nr;
+    pi = ni;
+  }
+}
+
+/* 2 * saturate(|y|) - 1, saturate(NaN) = 0 (am.cu:49, quad_demod.cu:47-48) */
+static inline float am_env(float re, float im) {
+  float m = hypotf(re, im);
+  m = (m > 0.0f) ? (m < 1.0f ? m : 1.0f) : 0.0f;
+  return 2.0f * m - 1.0f;
+}
+
+void oracle_am_demod(float fs, float tune, float chan, uint32_t D, uint64_t n0, const float* taps, size_t T,
+                     const float* x, float* out, size_t m0, size_t m1) {
+  const uint32_t inc = oracle_nco_inc(fs, tune, chan);
+  for (size_t m = m0; m < m1; ++m) {
+    float yr, yi;
+    chain_point(inc, D, n0, taps, T, x, m, &yr, &yi);
+    out[m] = am_env(yr, yi);
+  }
+}
+
+/* ---------------------------------------------------------------- A.2 quad demods, magnitude */
+
+void oracle_quad_fm(const float* x, float* out, float gain, size_t n) {
+  for (size_t k = 0; k < n; ++k) out[k] = disc(x[2 * k], x[2 * k + 1], x[2 * k + 2], x[2 * k + 3], gain);
+}
+
+void oracle_quad_am(const float* x, float* out, size_t n) {
+  for (size_t k = 0; k < n; ++k) out[k] = am_env(x[2 * k], x[2 * k + 1]);
+}
+
+void oracle_magnitude(const float* x, float* out, size_t n) {
+  for (size_t k = 0; k < n; ++k) out[k] = hypotf(x[2 * k], x[2 * k + 1]);
+}
+
+/* ---------------------------------------------------------------- A.5 QPSK */
+
+void oracle_qpsk_mod(const uint8_t* bits, float* out, uint32_t n, float a) {
+  for (uint32_t k = 0; k < n; ++k) {
+    const unsigned s = (bits[k >> 2] >> (2 * (k & 3))) & 3u;
+    out[2 * k] = (s & 1u) ? -a : a;
+    out[2 * k + 1] = (s & 2u) ? -a : a;
+  }
+}
+
+void oracle_qpsk_demod(const float* in, uint8_t* bits, uint32_t n) {
+  for (uint32_t k = 0; k < n; ++k) {
+    const unsigned s = (in[2 * k] >= 0.0f ? 0u : 1u) | (in[2 * k + 1] >= 0.0f ? 0u : 2u);
+    const unsigned sh = 2 * (k & 3);
+    bits[k >> 2] = (uint8_t)((bits[k >> 2] & ~(3u << sh)) | (s << sh));
+  }
+}
+
+/* ---------------------------------------------------------------- A.6 QPSK256 */
+
+void oracle_qpsk256_table(uint32_t type, float amplitude, float* t) {
+  if (type == 0) {
+    for (int i = 0; i < 16; ++i) {
+      for (int q = 0; q < 16; ++q) {
+        t[2 * (i * 16 + q)] = ((float)i - 7.5f) / 7.5f * amplitude;
+        t[2 * (i * 16 + q) + 1] = ((float)q - 7.5f) / 7.5f * amplitude;
+      }
+    }
+    return;
+  }
+  static const int kPoints[8] = {1, 8, 16, 24, 32, 40, 48, 56};
+  static const float kRadii[8] = {0.0f, 0.3f, 0.6f, 0.85f, 1.1f, 1.35f, 1.6f, 1.85f};
+  int idx = 0;
+  for (int c = 0; c < 8 && idx < 256; ++c) {
+    const int points = kPoints[c] < 256 - idx ? kPoints[c] : 256 - idx;
+    const float radius = kRadii[c] * amplitude;
+    for (int p = 0; p < points && idx < 256; ++p) {
+      const float angle = 2.0f * kPiF * (float)p / (float)points + ((float)c * 0.5f);
+      t[2 * idx] = radius * cosf(angle);
+      t[2 * idx + 1] = radius * sinf(angle);
+      ++idx;
+    }
+  }
+  while (idx < 256) {
+    const float angle = 2.0f * kPiF * (float)idx / 256.0f;
+    const float radius = amplitude * 0.95f;
+    t[2 * idx] = radius * cosf(angle);
+    t[2 * idx + 1] = radius * sinf(angle);
+    ++idx;
+  }
+}
+
+void oracle_qpsk256_mod(const float* table, const uint8_t* in, float* out, uint32_t n) {
+  for (uint32_t k = 0; k < n; ++k) {
+    out[2 * k] = table[2 * in[k]];
+    out[2 * k + 1] = table[2 * in[k] + 1];
+  }
+}
+
+void oracle_qpsk256_demod(const float* table, const float* in, uint8_t* out, uint32_t n) {
+  for (uint32_t k = 0; k < n; ++k) {
+    const float rx = in[2 * k], ry = in[2 * k + 1];
+    float best = INFINITY;
+    unsigned idx = 0;
+    for (unsigned i = 0; i < 256; ++i) {
+      const float dx = rx - table[2 * i];
+      const float dy = ry - table[2 * i + 1];
+      const float d = dx * dx + dy * dy;
+      if (d < best) {
+        best = d;
+        idx = i;
+      }
+    }
+    out[k] = (uint8_t)idx;
+  }
+}
+
+void oracle_qpsk256_demod_hypot(const float* table, const float* in, uint8_t* out, uint32_t n) {
+  for (uint32_t k = 0; k < n; ++k) {
+    const float rx = in[2 * k], ry = in[2 * k + 1];
+    float best = INFINITY;
+    unsigned idx = 0;
+    for (unsigned i = 0; i < 256; ++i) {
+      const float d = hypotf(rx - table[2 * i], ry - table[2 * i + 1]);
+      if (d < best) {
+        best = d;
+        idx = i;
+      }
+    }
+    out[k] = (uint8_t)idx;
+  }
+}

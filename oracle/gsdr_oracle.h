@@ -1,0 +1,78 @@
+/*
+ * gsdr CPU oracle -- TEST INFRASTRUCTURE ONLY.
+ *
+ * A scalar C restatement of the reference's hot-path semantics (kernrj/gsdr, read as text; the
+ * reference itself cannot be built here: it needs nvcc/CUDA and a CMake-generated gsdr_export.h).
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library, and
+ * only as the checker or the timed CPU baseline -- never as a product path.
+ *
+ * Parity pinning: see oracle/README.md and DESIGN.md section "Oracle". The oracle is checked against
+ * (a) the known-answer tests of the reference's gtest suite, re-encoded with the kernel's actual
+ * semantics, and (b) an independent float64 numpy restatement (tests/golden/). No executable output
+ * of the reference exists, so transcendental results (atan2f, hypotf, sincos) are pinned by tolerance.
+ *
+ * Complex arrays are interleaved float pairs (re, im), the layout of cuComplex / hipFloatComplex.
+ * Range arguments [k0, k1) select which outputs to compute, so full-size inputs can be spot-checked.
+ */
+#ifndef GSDR_ORACLE_H_
+#define GSDR_ORACLE_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* A.1 FIR, reference src/fir.cu:26-71: y[k] = sum_{i<T} x[k*D + i] * t[i], i ascending, fmaf per
+ * component, accumulator from zero (cuComplexOperatorOverloads.cuh:25-72). */
+void oracle_fir_ff(size_t D, const float* t, size_t T, const float* x, float* y, size_t k0, size_t k1);
+void oracle_fir_fc(size_t D, const float* t, size_t T, const float* x, float* y, size_t k0, size_t k1);
+void oracle_fir_cc(size_t D, const float* t, size_t T, const float* x, float* y, size_t k0, size_t k1);
+void oracle_fir_cf(size_t D, const float* t, size_t T, const float* x, float* y, size_t k0, size_t k1);
+
+/* Multi-threaded FC FIR over [0, N) (static split by output range) -- the CPU baseline. */
+void oracle_fir_fc_mt(size_t D, const float* t, size_t T, const float* x, float* y, size_t N, int nthreads);
+
+/* Condition bound S_k = sum_i |t_i| * |x_{kD+i}| (complex |.|), for the normwise parity metric. */
+void oracle_fir_bound_fc(size_t D, const float* t, size_t T, const float* x, float* s, size_t k0, size_t k1);
+
+/* A.3 NCO: inc = llround(fmod((tune - chan) / fs * 2^32, 2^32)) mod 2^32 (fm.cu:204, am.cu:68). */
+uint32_t oracle_nco_inc(float fs, float tune, float chan);
+/* z[n] = x[n] * exp(+j 2 pi P / 2^32), P = (uint32)((n0 + n) * inc), for n in [i0, i1). */
+void oracle_nco_mix(const float* x, float* z, uint64_t n0, uint32_t inc, size_t i0, size_t i1);
+
+/* A.4 FM chain (fm.cu:21-69, 181-218, re-specified): outputs m in [m0, m1), input N*D + T samples. */
+void oracle_fm_demod(float fs, float tune, float chan, float dev, uint32_t D, uint64_t n0, const float* taps,
+                     size_t T, const float* x, float* out, size_t m0, size_t m1);
+/* A.4 AM chain (am.cu:21-81): outputs m in [m0, m1). */
+void oracle_am_demod(float fs, float tune, float chan, uint32_t D, uint64_t n0, const float* taps, size_t T,
+                     const float* x, float* out, size_t m0, size_t m1);
+/* FIR stage of the chains (NCO-mixed, filtered), y[m] for m in [m0, m1): exposes the pre-discriminator
+ * signal for the normwise FIR check. */
+void oracle_chain_fir(float fs, float tune, float chan, uint32_t D, uint64_t n0, const float* taps, size_t T,
+                      const float* x, float* y, size_t m0, size_t m1);
+
+/* A.2 quad demods (quad_demod.cu:23-54) and magnitude (magnitude.cu:20-28). */
+void oracle_quad_fm(const float* x, float* out, float gain, size_t n);
+void oracle_quad_am(const float* x, float* out, size_t n);
+void oracle_magnitude(const float* x, float* out, size_t n);
+
+/* A.5 QPSK (qpsk.cu:108-146, 221-268). demod rewrites every byte holding one of the n symbols and
+ * preserves the unused high bit pairs of a final partial byte. */
+void oracle_qpsk_mod(const uint8_t* bits, float* out, uint32_t n, float a);
+void oracle_qpsk_demod(const float* in, uint8_t* bits, uint32_t n);
+
+/* A.6 QPSK256 (qpsk256.cu:29-71, 74-101, 154-195). table: 256 interleaved points. */
+void oracle_qpsk256_table(uint32_t type, float amplitude, float* table);
+void oracle_qpsk256_mod(const float* table, const uint8_t* in, float* out, uint32_t n);
+/* bit-exact contract: first index of min fl(fl(dx*dx) + fl(dy*dy)), strict <, init +inf */
+void oracle_qpsk256_demod(const float* table, const float* in, uint8_t* out, uint32_t n);
+/* the reference's literal rule with hypotf in place of cuCabsf (non-gating cross-check) */
+void oracle_qpsk256_demod_hypot(const float* table, const float* in, uint8_t* out, uint32_t n);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GSDR_ORACLE_H_ */

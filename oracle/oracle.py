@@ -1,0 +1,201 @@
+"""ctypes binding of the C oracle (oracle/gsdr_oracle.c) for numpy arrays -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module, and
+only as the checker or as the timed CPU baseline. Complex arrays are numpy complex64 (interleaved
+float pairs, the hipFloatComplex layout).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "build", "liboracle.so")
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f"{LIB_PATH} missing: run `make oracle/build/liboracle.so`")
+_lib = ctypes.CDLL(LIB_PATH)
+
+_p, _sz, _u32, _u64, _f, _int = (ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint64,
+                                 ctypes.c_float, ctypes.c_int)
+_SIG = {
+    "oracle_fir_ff": [_sz, _p, _sz, _p, _p, _sz, _sz],
+    "oracle_fir_fc": [_sz, _p, _sz, _p, _p, _sz, _sz],
+    "oracle_fir_cc": [_sz, _p, _sz, _p, _p, _sz, _sz],
+    "oracle_fir_cf": [_sz, _p, _sz, _p, _p, _sz, _sz],
+    "oracle_fir_fc_mt": [_sz, _p, _sz, _p, _p, _sz, _int],
+    "oracle_fir_bound_fc": [_sz, _p, _sz, _p, _p, _sz, _sz],
+    "oracle_nco_mix": [_p, _p, _u64, _u32, _sz, _sz],
+    "oracle_fm_demod": [_f, _f, _f, _f, _u32, _u64, _p, _sz, _p, _p, _sz, _sz],
+    "oracle_am_demod": [_f, _f, _f, _u32, _u64, _p, _sz, _p, _p, _sz, _sz],
+    "oracle_chain_fir": [_f, _f, _f, _u32, _u64, _p, _sz, _p, _p, _sz, _sz],
+    "oracle_quad_fm": [_p, _p, _f, _sz],
+    "oracle_quad_am": [_p, _p, _sz],
+    "oracle_magnitude": [_p, _p, _sz],
+    "oracle_qpsk_mod": [_p, _p, _u32, _f],
+    "oracle_qpsk_demod": [_p, _p, _u32],
+    "oracle_qpsk256_table": [_u32, _f, _p],
+    "oracle_qpsk256_mod": [_p, _p, _p, _u32],
+    "oracle_qpsk256_demod": [_p, _p, _p, _u32],
+    "oracle_qpsk256_demod_hypot": [_p, _p, _p, _u32],
+}
+for _name, _args in _SIG.items():
+    getattr(_lib, _name).argtypes = _args
+    getattr(_lib, _name).restype = None
+_lib.oracle_nco_inc.argtypes = [_f, _f, _f]
+_lib.oracle_nco_inc.restype = _u32
+
+
+def _c(a, dtype):
+    a = np.ascontiguousarray(a, dtype=dtype)
+    return a
+
+
+def _ptr(a):
+    return a.ctypes.data
+
+
+_FIR = {
+    (np.float32, np.float32): ("oracle_fir_ff", np.float32),
+    (np.float32, np.complex64): ("oracle_fir_fc", np.complex64),
+    (np.complex64, np.complex64): ("oracle_fir_cc", np.complex64),
+    (np.complex64, np.float32): ("oracle_fir_cf", np.complex64),
+}
+
+
+def fir(taps, x, decimation=1, num_outputs=None, k0=0, k1=None):
+    """y[k] for k in [k0, k1) (other entries zero). Dtypes pick FF/FC/CC/CF like the C ABI."""
+    taps = np.ascontiguousarray(taps)
+    x = np.ascontiguousarray(x)
+    name, odt = _FIR[(taps.dtype.type, x.dtype.type)]
+    T = taps.size
+    if num_outputs is None:
+        num_outputs = (x.size - T) // decimation + 1
+    k1 = num_outputs if k1 is None else k1
+    assert x.size >= (k1 - 1) * decimation + T if k1 > 0 else True
+    y = np.zeros(num_outputs, dtype=odt)
+    getattr(_lib, name)(decimation, _ptr(taps), T, _ptr(x), _ptr(y), k0, k1)
+    return y
+
+
+def fir_fc_mt(taps, x, decimation, num_outputs, nthreads):
+    taps = _c(taps, np.float32)
+    x = _c(x, np.complex64)
+    y = np.empty(num_outputs, dtype=np.complex64)
+    _lib.oracle_fir_fc_mt(decimation, _ptr(taps), taps.size, _ptr(x), _ptr(y), num_outputs, nthreads)
+    return y
+
+
+def fir_bound_fc(taps, x, decimation, num_outputs, k0=0, k1=None):
+    taps = _c(taps, np.float32)
+    x = _c(x, np.complex64)
+    k1 = num_outputs if k1 is None else k1
+    s = np.zeros(num_outputs, dtype=np.float32)
+    _lib.oracle_fir_bound_fc(decimation, _ptr(taps), taps.size, _ptr(x), _ptr(s), k0, k1)
+    return s
+
+
+def nco_inc(fs, tune, chan):
+    return int(_lib.oracle_nco_inc(fs, tune, chan))
+
+
+def nco_mix(x, n0, inc):
+    x = _c(x, np.complex64)
+    z = np.empty_like(x)
+    _lib.oracle_nco_mix(_ptr(x), _ptr(z), n0, inc, 0, x.size)
+    return z
+
+
+def fm_demod(x, taps, fs, tune, chan, dev, decimation, first_sample_index=0, num_outputs=None, m0=0, m1=None):
+    x = _c(x, np.complex64)
+    taps = _c(taps, np.float32)
+    if num_outputs is None:
+        num_outputs = (x.size - taps.size) // decimation
+    m1 = num_outputs if m1 is None else m1
+    out = np.zeros(num_outputs, dtype=np.float32)
+    _lib.oracle_fm_demod(fs, tune, chan, dev, decimation, first_sample_index, _ptr(taps), taps.size, _ptr(x),
+                         _ptr(out), m0, m1)
+    return out
+
+
+def am_demod(x, taps, fs, tune, chan, decimation, first_sample_index=0, num_outputs=None, m0=0, m1=None):
+    x = _c(x, np.complex64)
+    taps = _c(taps, np.float32)
+    if num_outputs is None:
+        num_outputs = (x.size - taps.size) // decimation + 1
+    m1 = num_outputs if m1 is None else m1
+    out = np.zeros(num_outputs, dtype=np.float32)
+    _lib.oracle_am_demod(fs, tune, chan, decimation, first_sample_index, _ptr(taps), taps.size, _ptr(x),
+                         _ptr(out), m0, m1)
+    return out
+
+
+def chain_fir(x, taps, fs, tune, chan, decimation, first_sample_index, num_outputs, m0=0, m1=None):
+    x = _c(x, np.complex64)
+    taps = _c(taps, np.float32)
+    m1 = num_outputs if m1 is None else m1
+    y = np.zeros(num_outputs, dtype=np.complex64)
+    _lib.oracle_chain_fir(fs, tune, chan, decimation, first_sample_index, _ptr(taps), taps.size, _ptr(x), _ptr(y),
+                          m0, m1)
+    return y
+
+
+def quad_fm(x, gain, n=None):
+    x = _c(x, np.complex64)
+    n = x.size - 1 if n is None else n
+    out = np.empty(n, dtype=np.float32)
+    _lib.oracle_quad_fm(_ptr(x), _ptr(out), gain, n)
+    return out
+
+
+def quad_am(x):
+    x = _c(x, np.complex64)
+    out = np.empty(x.size, dtype=np.float32)
+    _lib.oracle_quad_am(_ptr(x), _ptr(out), x.size)
+    return out
+
+
+def magnitude(x):
+    x = _c(x, np.complex64)
+    out = np.empty(x.size, dtype=np.float32)
+    _lib.oracle_magnitude(_ptr(x), _ptr(out), x.size)
+    return out
+
+
+def qpsk_mod(bits, n, a):
+    bits = _c(bits, np.uint8)
+    assert bits.size >= (n + 3) // 4
+    out = np.empty(n, dtype=np.complex64)
+    _lib.oracle_qpsk_mod(_ptr(bits), _ptr(out), n, a)
+    return out
+
+
+def qpsk_demod(x, n=None, initial=None):
+    x = _c(x, np.complex64)
+    n = x.size if n is None else n
+    bits = np.zeros((n + 3) // 4, dtype=np.uint8) if initial is None else np.array(initial, dtype=np.uint8)
+    _lib.oracle_qpsk_demod(_ptr(x), _ptr(bits), n)
+    return bits
+
+
+def qpsk256_table(ctype, amplitude):
+    t = np.empty(256, dtype=np.complex64)
+    _lib.oracle_qpsk256_table(ctype, amplitude, _ptr(t))
+    return t
+
+
+def qpsk256_mod(table, symbols):
+    table = _c(table, np.complex64)
+    symbols = _c(symbols, np.uint8)
+    out = np.empty(symbols.size, dtype=np.complex64)
+    _lib.oracle_qpsk256_mod(_ptr(table), _ptr(symbols), _ptr(out), symbols.size)
+    return out
+
+
+def qpsk256_demod(table, x, rule="sq"):
+    table = _c(table, np.complex64)
+    x = _c(x, np.complex64)
+    out = np.empty(x.size, dtype=np.uint8)
+    fn = _lib.oracle_qpsk256_demod if rule == "sq" else _lib.oracle_qpsk256_demod_hypot
+    fn(_ptr(table), _ptr(x), _ptr(out), x.size)
+    return out

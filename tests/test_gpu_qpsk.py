@@ -1,0 +1,184 @@
+"""GPU parity, bit-exact: QPSK (reference src/qpsk.cu) and QPSK256 (src/qpsk256.cu) through the C ABI
+vs the C oracle. Named after the reference's tests/test_qpsk.cpp and tests/test_qpsk256.cpp cases."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as o
+
+pytestmark = pytest.mark.gpu
+
+
+def dev(a, cuda):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(cuda)
+
+
+NS = [1, 3, 4, 5, 15, 16, 17, 31, 33, 1001, 65536 + 3]
+
+
+def noisy_qpsk(bits, n, a, seed):
+    sym = o.qpsk_mod(bits, n, a)
+    rng = np.random.default_rng(seed)
+    rx = (sym + 0.4 * a * (rng.standard_normal(n) + 1j * rng.standard_normal(n))).astype(np.complex64)
+    rx[: min(n, 3)] = [0.0, complex(-0.0, -0.0), complex(np.nan, 1.0)][: min(n, 3)]
+    return sym, rx
+
+
+@pytest.mark.parametrize("n", NS)
+def test_qpsk_modulate_demodulate(cuda, n):
+    from gsdr_amd import ops
+
+    rng = np.random.default_rng(n)
+    bits = rng.integers(0, 256, (n + 3) // 4, dtype=np.uint8)
+    sym = ops.qpsk_modulate(dev(bits, cuda), n, 0.8)
+    ref_sym, rx = noisy_qpsk(bits, n, 0.8, n)
+    assert np.array_equal(sym.cpu().numpy(), ref_sym)
+    # demod: bytes pre-filled with 0xff so the preserved high pairs of a final partial byte show
+    prev = np.full((n + 3) // 4, 0xFF, dtype=np.uint8)
+    got = dev(prev, cuda)
+    ops.qpsk_demodulate(dev(rx, cuda), n, out=got)
+    torch.cuda.synchronize()
+    assert np.array_equal(got.cpu().numpy(), o.qpsk_demod(rx, n, initial=prev))
+
+
+def test_qpsk_round_trip_and_points(cuda):
+    """test_qpsk.cpp:87-170: ideal-channel round trip, four points, |.| = a sqrt 2."""
+    from gsdr_amd import ops
+
+    n = 100003
+    bits = np.random.default_rng(1).integers(0, 256, (n + 3) // 4, dtype=np.uint8)
+    for a in (0.5, 1.0, 2.0, 10.0):
+        sym = ops.qpsk_modulate(dev(bits, cuda), n, a)
+        back = ops.qpsk_demodulate(sym).cpu().numpy()
+        s = sym.cpu().numpy()
+        assert set(np.unique(s).tolist()) == {complex(a, a), complex(-a, a), complex(-a, -a), complex(a, -a)}
+        last = n % 4
+        full = n // 4
+        assert np.array_equal(back[:full], bits[:full])
+        if last:
+            mask = (1 << (2 * last)) - 1
+            assert (back[full] & mask) == (bits[full] & mask)
+
+
+def test_qpsk_4x(cuda):
+    from gsdr_amd import ops
+
+    n = 4099
+    rng = np.random.default_rng(2)
+    bits = [rng.integers(0, 256, (n + 3) // 4, dtype=np.uint8) for _ in range(4)]
+    outs = [torch.empty(n, dtype=torch.complex64, device=cuda) for _ in range(4)]
+    ops.qpsk_modulate_4x([dev(b, cuda) for b in bits], outs, n, 1.5)
+    rx = [noisy_qpsk(bits[i], n, 1.5, 10 + i)[1] for i in range(4)]
+    got = [torch.zeros((n + 3) // 4, dtype=torch.uint8, device=cuda) for _ in range(4)]
+    ops.qpsk_demodulate_4x([dev(r, cuda) for r in rx], got, n)
+    torch.cuda.synchronize()
+    for i in range(4):
+        assert np.array_equal(outs[i].cpu().numpy(), o.qpsk_mod(bits[i], n, 1.5))
+        assert np.array_equal(got[i].cpu().numpy(), o.qpsk_demod(rx[i], n))
+
+
+@pytest.mark.parametrize("streams", [1, 2, 3, 4, 8])
+@pytest.mark.parametrize("n", [5, 1001, 4096])
+def test_qpsk_templated(cuda, streams, n):
+    """Consolidated layout (qpsk.cu:42, 56, 75, 87): bits at s*(n/4+1), symbols at s*n; unsupported
+    stream counts fall back to stream 0 only (qpsk.cu:619-622)."""
+    from gsdr_amd import ops
+
+    S = 8
+    stride = n // 4 + 1
+    rng = np.random.default_rng(n + streams)
+    bits = rng.integers(0, 256, S * stride, dtype=np.uint8)
+    out = torch.zeros(S * n, dtype=torch.complex64, device=cuda)
+    ops.qpsk_modulate_templated(dev(bits, cuda), out, n, 1.0, streams)
+    active = streams if streams in (1, 2, 4, 8) else 1
+    rx = np.concatenate([noisy_qpsk(bits[s * stride:(s + 1) * stride], n, 1.0, s)[1] for s in range(S)])
+    got = torch.full((S * stride,), 0xAA, dtype=torch.uint8, device=cuda)
+    ops.qpsk_demodulate_templated(dev(rx, cuda), got, n, streams)
+    torch.cuda.synchronize()
+    o_sym = out.cpu().numpy()
+    g = got.cpu().numpy()
+    for s in range(S):
+        b = bits[s * stride:(s + 1) * stride]
+        if s < active:
+            assert np.array_equal(o_sym[s * n:(s + 1) * n], o.qpsk_mod(b, n, 1.0))
+            want = o.qpsk_demod(rx[s * n:(s + 1) * n], n, initial=np.full(stride, 0xAA, np.uint8))
+            assert np.array_equal(g[s * stride:(s + 1) * stride], want)
+        else:
+            assert np.all(o_sym[s * n:(s + 1) * n] == 0)
+            assert np.all(g[s * stride:(s + 1) * stride] == 0xAA)
+
+
+# ------------------------------------------------------------------------------------ QPSK256
+
+@pytest.mark.parametrize("ctype", [0, 1])
+@pytest.mark.parametrize("amp", [1.0, 0.5, 2.5])
+def test_qpsk256_tables_and_modulate(cuda, ctype, amp):
+    """test_qpsk256.cpp:128-170: 256 distinct points; the device table equals the oracle's bitwise."""
+    from gsdr_amd import ops
+
+    ops.qpsk256_init(ctype, amp)
+    syms = np.arange(256, dtype=np.uint8)
+    pts = ops.qpsk256_modulate(dev(syms, cuda), ctype).cpu().numpy()
+    assert np.array_equal(pts, o.qpsk256_table(ctype, amp))
+    assert len(set(pts.tolist())) == 256
+
+
+@pytest.mark.parametrize("ctype,sigma", [(0, 0.02), (0, 0.08), (1, 0.01)])
+@pytest.mark.parametrize("n", [1, 15, 16, 17, 100003])
+def test_qpsk256_demodulate_bit_exact(cuda, ctype, sigma, n):
+    from gsdr_amd import ops
+
+    amp = 1.0
+    ops.qpsk256_init(ctype, amp)
+    table = o.qpsk256_table(ctype, amp)
+    rng = np.random.default_rng(n + ctype)
+    syms = rng.integers(0, 256, n, dtype=np.uint8)
+    rx = (table[syms] + sigma * (rng.standard_normal(n) + 1j * rng.standard_normal(n))).astype(np.complex64)
+    special = [complex(np.nan, 0), complex(np.inf, 1), complex(1e30, -1e30), complex(7.5, -7.5), 0j,
+               complex(1.0 / 15.0, 1.0 / 15.0)]  # last: an exact midpoint between two grid levels
+    rx[: min(n, len(special))] = special[: min(n, len(special))]
+    got = ops.qpsk256_demodulate(dev(rx, cuda), ctype).cpu().numpy()
+    assert np.array_equal(got, o.qpsk256_demod(table, rx))
+
+
+def test_qpsk256_4x(cuda):
+    from gsdr_amd import ops
+
+    n, ctype = 5003, 0
+    ops.qpsk256_init(ctype, 1.0)
+    table = o.qpsk256_table(ctype, 1.0)
+    rng = np.random.default_rng(44)
+    syms = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(4)]
+    outs = [torch.empty(n, dtype=torch.complex64, device=cuda) for _ in range(4)]
+    ops.qpsk256_modulate_4x([dev(s, cuda) for s in syms], outs, n, ctype)
+    back = [torch.empty(n, dtype=torch.uint8, device=cuda) for _ in range(4)]
+    ops.qpsk256_demodulate_4x(outs, back, n, ctype)
+    torch.cuda.synchronize()
+    for i in range(4):
+        assert np.array_equal(outs[i].cpu().numpy(), table[syms[i]])
+        assert np.array_equal(back[i].cpu().numpy(), syms[i])
+
+
+def test_qpsk256_config5_round_trip(cuda):
+    """BASELINE config 5: 2^24 symbols, rectangular, a = 1, AWGN sigma = 0.02 per axis. GPU demod is
+    compared bit for bit with the oracle on 1 M of the noisy symbols (the oracle's 256-way search is
+    the slow side); the symbol error rate vs the transmitted bytes is a sanity figure only."""
+    from gsdr_amd import ops
+
+    n, ctype = 1 << 24, 0
+    ops.qpsk256_init(ctype, 1.0)
+    g = torch.Generator(device=cuda).manual_seed(0x5EED)
+    syms = torch.randint(0, 256, (n,), dtype=torch.uint8, device=cuda, generator=g)
+    tx = ops.qpsk256_modulate(syms, ctype)
+    noise = torch.randn(n, dtype=torch.complex64, device=cuda, generator=g) * (0.02 * np.sqrt(2.0))
+    rx = tx + noise
+    got = ops.qpsk256_demodulate(rx, ctype)
+    torch.cuda.synchronize()
+    ser = float((got != syms).float().mean())
+    assert 1e-5 < ser < 1e-2
+    table = o.qpsk256_table(ctype, 1.0)
+    rx_np = rx.cpu().numpy()
+    got_np = got.cpu().numpy()
+    for k0 in (0, n // 2, n - (1 << 18)):
+        k1 = k0 + (1 << 18)
+        assert np.array_equal(got_np[k0:k1], o.qpsk256_demod(table, rx_np[k0:k1]))

@@ -4,7 +4,7 @@ CC      ?= gcc
 ARCH    ?= gfx950
 BUILD   := build
 
-HIPFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -fvisibility=hidden -fvisibility-inlines-hidden \
+HIPFLAGS := -O3 -std=c++17 -fPIC -ffp-contract=off --offload-arch=$(ARCH) -fvisibility=hidden -fvisibility-inlines-hidden \
             -Wall -Wno-unused-function -Iinclude -Igsdr_amd/csrc -munsafe-fp-atomics
 # Oracle: explicit fmaf where the spec says FMA, no implicit contraction.
 OFLAGS  := -O2 -std=c11 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wextra -Ioracle -mfma
@@ -18,6 +18,11 @@ all: gsdr_amd/libgsdr.so oracle/build/liboracle.so
 $(BUILD)/%.o: gsdr_amd/csrc/%.hip $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+# tuning probes: scalar-FMA build of the headline kernel (see fir_probe.hip)
+$(BUILD)/fir_probe.o: gsdr_amd/csrc/fir_probe.hip $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -fno-slp-vectorize -c $< -o $@
 
 gsdr_amd/libgsdr.so: $(OBJS)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -Wl,-rpath,/opt/rocm/lib $(OBJS) -o $@

@@ -58,7 +58,7 @@ hipError_t launch_generic(const FirJob& j, hipStream_t s) {
   return launch_status();
 }
 
-template <class TapT, class InT, int D, int R, int JC, int WG, int MODE>
+template <class TapT, class InT, int D, int R, int JC, int WG, int MODE, int ABL = 0>
 hipError_t launch_poly(const FirJob& j, hipStream_t s) {
   using Geo = TileGeo<InT, D, R, WG>;
   FirParams p = make_params(j);
@@ -75,9 +75,9 @@ hipError_t launch_poly(const FirJob& j, hipStream_t s) {
   if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
   const bool vec = aligned16(j.in) && ((uint64_t)stride * D * sizeof(InT)) % 16 == 0;
   if (vec) {
-    k_fir_poly<TapT, InT, D, R, JC, WG, true, MODE><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
+    k_fir_poly<TapT, InT, D, R, JC, WG, true, MODE, ABL><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
   } else {
-    k_fir_poly<TapT, InT, D, R, JC, WG, false, MODE><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
+    k_fir_poly<TapT, InT, D, R, JC, WG, false, MODE, ABL><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
   }
   return launch_status();
 }
@@ -107,8 +107,12 @@ hipError_t launch_contig(const FirJob& j, hipStream_t s) {
 
 // Tile-shape variants of the headline case (real taps, complex input, D = 4), selectable through
 // gsdrxFirFCVariant for tuning sweeps. Variant 0 is the default.
+// Tuning probes (variant >= 100) live in fir_probe.hip, compiled separately.
+hipError_t launch_fc_probe(const FirJob& j, hipStream_t s);
+
 template <class TapT, class InT, int MODE>
 hipError_t launch_d4_complex(const FirJob& j, hipStream_t s) {
+  if (j.variant >= 100) return launch_fc_probe(j, s);
   switch (j.variant) {
     case 1:
       return launch_poly<TapT, InT, 4, 4, 16, 256, MODE>(j, s);

@@ -318,7 +318,8 @@ __device__ __forceinline__ void tile_epilogue(const FirParams& p, uint64_t out0,
 // Kernel 1: polyphase-granule kernel, D a multiple of the granule width G.
 //   JC = tap rows per chunk (a multiple of R); a chunk covers JC*D taps.
 // ------------------------------------------------------------------------------------------------
-template <class TapT, class InT, int D, int R, int JC, int WG, bool VEC, int MODE>
+// ABL (ablation, tuning probes only): 0 = full kernel, 1 = staging only, 2 = compute only.
+template <class TapT, class InT, int D, int R, int JC, int WG, bool VEC, int MODE, int ABL = 0>
 __global__ __launch_bounds__(WG) void k_fir_poly(FirParams p) {
   using Geo = TileGeo<InT, D, R, WG>;
   using OutT = typename Product<TapT, InT>::type;
@@ -337,7 +338,7 @@ __global__ __launch_bounds__(WG) void k_fir_poly(FirParams p) {
   const uint32_t span = p.nch * JC * D;
   const uint32_t NG = ((Geo::KT - 1) * D + span + G - 1) / G;
 
-  stage_tile<InT, Geo, WG, VEC, MODE>(lds, in, S0, NG, p);
+  if constexpr (ABL != 2) stage_tile<InT, Geo, WG, VEC, MODE>(lds, in, S0, NG, p);
   __syncthreads();
 
   OutT acc[R];
@@ -345,7 +346,12 @@ __global__ __launch_bounds__(WG) void k_fir_poly(FirParams p) {
   for (int r = 0; r < R; ++r) set_zero(acc[r]);
 
   const uint32_t t = threadIdx.x;
-  for (uint32_t c = 0; c < p.nch; ++c) {
+  if constexpr (ABL == 1) {
+    const float4 v = lds[Geo::padded(t * Geo::SG)];
+#pragma unroll
+    for (int r = 0; r < R; ++r) mac(acc[r], granule_sample<InT>(v, r % G), 1.0f);
+  }
+  for (uint32_t c = 0; c < (ABL == 1 ? 0u : p.nch); ++c) {
     const float4* __restrict__ seg = lds + (t + c * (JC / R)) * Geo::SGP;
 #pragma unroll
     for (int h = 0; h < CPR; ++h) {

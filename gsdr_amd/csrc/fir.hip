@@ -37,6 +37,70 @@ static hipError_t fir_entry(size_t decimation, const TapT* taps, size_t tapCount
                  })());
 }
 
+// Streaming ceiling probe for this traffic mix: reads the 8*N_in input bytes with fully coalesced
+// 16-byte loads and writes 8*N_out bytes (outputs are a sum of loaded samples, not a FIR).
+template <bool NT>
+__global__ __launch_bounds__(256) void k_stream_probe(const float4* __restrict__ in, float4* __restrict__ out,
+                                                      uint64_t n_in16, uint64_t n_out16) {
+  // each thread: 4 input granules (one per 1 KiB wave-slab) -> 1 output granule
+  const uint64_t wave = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 6;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t o = wave * 64u + lane;
+  if (o >= n_out16) return;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint64_t i = (wave * 4u + k) * 64u + lane;
+    if (i < n_in16) {
+      const float4 v = NT ? load16_nt(in + i) : in[i];
+      a.x += v.x;
+      a.y += v.y;
+      a.z += v.z;
+      a.w += v.w;
+    }
+  }
+  out[o] = a;
+}
+
+hipError_t launch_stream_probe(const FirJob& j, hipStream_t s, bool nt) {
+  const uint64_t n_in16 = j.L * 8 / 16, n_out16 = j.N * 8 / 16;
+  const uint32_t blocks = (uint32_t)ceil_div<uint64_t>(n_out16, 256);
+  if (nt) {
+    k_stream_probe<true><<<blocks, 256, 0, s>>>(reinterpret_cast<const float4*>(j.in),
+                                                reinterpret_cast<float4*>(j.out), n_in16, n_out16);
+  } else {
+    k_stream_probe<false><<<blocks, 256, 0, s>>>(reinterpret_cast<const float4*>(j.in),
+                                                 reinterpret_cast<float4*>(j.out), n_in16, n_out16);
+  }
+  return launch_status();
+}
+
+// Packed-FMA tuning probes (gsdrxFirFCVariant 103+): 103 compute-only at the default shape,
+// 104 compute-only / 105 staging-only at the WG=256, R=4 shape.
+hipError_t launch_fc_probe_packed(const FirJob& j, hipStream_t s) {
+  switch (j.variant) {
+    case 103:
+      return launch_poly<float, float2, 4, 8, 16, 128, kModeFir, 2>(j, s);
+    case 104:
+      return launch_poly<float, float2, 4, 4, 16, 256, kModeFir, 2>(j, s);
+    case 105:
+      return launch_poly<float, float2, 4, 4, 16, 256, kModeFir, 1>(j, s);
+    case 106:  // WG=256, R=4 with non-temporal input loads
+      return launch_poly<float, float2, 4, 4, 16, 256, kModeFir, 0, true>(j, s);
+    case 107:  // staging only, non-temporal
+      return launch_poly<float, float2, 4, 4, 16, 256, kModeFir, 1, true>(j, s);
+    case 108:  // WG=512, R=2 (more waves, smaller windows)
+      return launch_poly<float, float2, 4, 2, 16, 512, kModeFir>(j, s);
+    case 109:  // WG=128, R=4
+      return launch_poly<float, float2, 4, 4, 16, 128, kModeFir>(j, s);
+    case 110:
+    case 111:
+      return launch_stream_probe(j, s, j.variant == 111);
+    default:
+      return hipErrorInvalidValue;
+  }
+}
+
 }  // namespace gsdr
 
 using gsdr::fir_entry;

@@ -9,6 +9,9 @@
 
 #include <hip/hip_runtime.h>
 
+#include <stdio.h>
+#include <stdlib.h>
+
 #include <type_traits>
 
 #include "fir_engine.hpp"
@@ -58,7 +61,7 @@ hipError_t launch_generic(const FirJob& j, hipStream_t s) {
   return launch_status();
 }
 
-template <class TapT, class InT, int D, int R, int JC, int WG, int MODE, int ABL = 0>
+template <class TapT, class InT, int D, int R, int JC, int WG, int MODE, int ABL = 0, bool NT = false>
 hipError_t launch_poly(const FirJob& j, hipStream_t s) {
   using Geo = TileGeo<InT, D, R, WG>;
   FirParams p = make_params(j);
@@ -75,9 +78,9 @@ hipError_t launch_poly(const FirJob& j, hipStream_t s) {
   if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
   const bool vec = aligned16(j.in) && ((uint64_t)stride * D * sizeof(InT)) % 16 == 0;
   if (vec) {
-    k_fir_poly<TapT, InT, D, R, JC, WG, true, MODE, ABL><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
+    k_fir_poly<TapT, InT, D, R, JC, WG, true, MODE, ABL, NT><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
   } else {
-    k_fir_poly<TapT, InT, D, R, JC, WG, false, MODE, ABL><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
+    k_fir_poly<TapT, InT, D, R, JC, WG, false, MODE, ABL, NT><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
   }
   return launch_status();
 }
@@ -105,17 +108,71 @@ hipError_t launch_contig(const FirJob& j, hipStream_t s) {
   return launch_status();
 }
 
+// Workgroups per CU that the hardware keeps resident for `kernel` at `lds` bytes (occupancy query,
+// capped by the LDS budget), times the CU count: the persistent grid.
+inline uint32_t persistent_grid(const void* kernel, int wg, size_t lds, int oversubscribe) {
+  int dev = 0, cus = 0, per_cu = 0, lds_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess) {
+    lds_cu = 160 * 1024;
+  }
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, wg, lds) != hipSuccess) return 0;
+  const int by_lds = lds > 0 ? (int)((size_t)lds_cu / lds) : per_cu;
+  if (by_lds < per_cu) per_cu = by_lds;
+  if (per_cu < 1) per_cu = 1;
+  const uint32_t grid = (uint32_t)(cus * per_cu * (oversubscribe < 1 ? 1 : oversubscribe));
+  static bool debug = getenv("GSDR_DEBUG") != nullptr;
+  if (debug) {
+    fprintf(stderr, "gsdr: persistent grid %u = %d CUs x %d WG/CU x %d (wg %d, lds %zu B, lds/CU %d)\n", grid, cus,
+            per_cu, oversubscribe, wg, lds, lds_cu);
+  }
+  return grid;
+}
+
+// Persistent, register-prefetching polyphase kernel (k_fir_poly_pipe). Falls back to the one-tile
+// kernel when the halo does not fit the HALO registers per thread.
+template <class TapT, class InT, int D, int R, int JC, int WG, int HALO, int MODE>
+hipError_t launch_poly_pipe(const FirJob& j, hipStream_t s, int oversubscribe = 1) {
+  using Geo = TileGeo<InT, D, R, WG>;
+  FirParams p = make_params(j);
+  const uint64_t rows = ceil_div<uint64_t>(j.T, (uint64_t)D);
+  const uint64_t nch = ceil_div<uint64_t>(rows, (uint64_t)JC);
+  const uint64_t span = nch * JC * D;
+  const uint64_t NG = ((uint64_t)(Geo::KT - 1) * D + span + Geo::G - 1) / Geo::G;
+  if (NG > (uint64_t)(Geo::SG + HALO) * WG) return launch_poly<TapT, InT, D, R, JC, WG, MODE>(j, s);
+  const size_t lds = poly_lds_bytes<InT, D, R, WG>((uint32_t)span, MODE);
+  if (lds > kMaxTileLds) return launch_generic<TapT, InT, MODE>(j, s);
+  p.nch = (uint32_t)nch;
+  const uint32_t stride = (MODE == kModeFm) ? Geo::KT - 1 : Geo::KT;
+  p.tile_stride = stride;
+  const uint64_t tiles = ceil_div<uint64_t>(j.N, stride);
+  if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
+  const bool vec = aligned16(j.in) && ((uint64_t)stride * D * sizeof(InT)) % 16 == 0;
+  if (!vec) return launch_poly<TapT, InT, D, R, JC, WG, MODE>(j, s);
+  const void* kern = reinterpret_cast<const void*>(&k_fir_poly_pipe<TapT, InT, D, R, JC, WG, HALO, MODE>);
+  uint32_t grid = persistent_grid(kern, WG, lds, oversubscribe);
+  if (grid == 0) return hipErrorInvalidDevice;
+  if (grid > tiles) grid = (uint32_t)tiles;
+  k_fir_poly_pipe<TapT, InT, D, R, JC, WG, HALO, MODE><<<dim3(grid), dim3(WG), lds, s>>>(p, (uint32_t)tiles);
+  return launch_status();
+}
+
 // Tile-shape variants of the headline case (real taps, complex input, D = 4), selectable through
-// gsdrxFirFCVariant for tuning sweeps. Variant 0 is the default.
-// Tuning probes (variant >= 100) live in fir_probe.hip, compiled separately.
+// gsdrxFirFCVariant for tuning sweeps. Variant 0 is the default (WG = 256, R = 4, JC = 16);
+// variant 1 is the round-1 starting shape (WG = 128, R = 8).
+// Tuning probes (variant >= 100): 100-102 live in fir_probe.hip (compiled with -fno-slp-vectorize),
+// 103+ in fir.hip (packed-FMA build).
 hipError_t launch_fc_probe(const FirJob& j, hipStream_t s);
+hipError_t launch_fc_probe_packed(const FirJob& j, hipStream_t s);
 
 template <class TapT, class InT, int MODE>
 hipError_t launch_d4_complex(const FirJob& j, hipStream_t s) {
+  if (j.variant >= 103) return launch_fc_probe_packed(j, s);
   if (j.variant >= 100) return launch_fc_probe(j, s);
   switch (j.variant) {
     case 1:
-      return launch_poly<TapT, InT, 4, 4, 16, 256, MODE>(j, s);
+      return launch_poly<TapT, InT, 4, 8, 16, 128, MODE>(j, s);
     case 2:
       return launch_poly<TapT, InT, 4, 8, 16, 256, MODE>(j, s);
     case 3:
@@ -128,8 +185,16 @@ hipError_t launch_d4_complex(const FirJob& j, hipStream_t s) {
       return launch_poly<TapT, InT, 4, 16, 16, 128, MODE>(j, s);
     case 7:
       return launch_generic<TapT, InT, MODE>(j, s);
+    case 20:
+      return launch_poly_pipe<TapT, InT, 4, 4, 16, 256, 1, MODE>(j, s);
+    case 21:
+      return launch_poly_pipe<TapT, InT, 4, 4, 8, 256, 1, MODE>(j, s);
+    case 22:
+      return launch_poly_pipe<TapT, InT, 4, 4, 16, 128, 1, MODE>(j, s);
+    case 23:
+      return launch_poly_pipe<TapT, InT, 4, 4, 16, 256, 1, MODE>(j, s, 2);
     default:
-      return launch_poly<TapT, InT, 4, 8, 16, 128, MODE>(j, s);
+      return launch_poly<TapT, InT, 4, 4, 16, 256, MODE>(j, s);
   }
 }
 
@@ -148,7 +213,8 @@ hipError_t launch_fir(const FirJob& j, hipStream_t s) {
         if constexpr (MODE == kModeFir && std::is_same<TapT, float>::value) {
           if (j.variant >= 0) return launch_d4_complex<TapT, InT, MODE>(j, s);
         }
-        return launch_poly<TapT, InT, 4, 8, 16, 128, MODE>(j, s);
+        // 4 waves/SIMD (16 per CU): the shape that measured fastest at T = 127
+        return launch_poly<TapT, InT, 4, 4, 16, 256, MODE>(j, s);
       case 8:
         return launch_poly<TapT, InT, 8, 8, 8, 128, MODE>(j, s);
       default:

@@ -95,23 +95,28 @@ struct TapBuf {
   gsdr_v4i32 rsrc;
 };
 
-__device__ __forceinline__ TapBuf make_tapbuf(const void* taps, uint32_t bytes) {
-  const uint64_t a = reinterpret_cast<uint64_t>(taps);
+// A window of the tap array starting at tap `base` (wave-uniform): the descriptor is re-based so
+// every tap inside the window is an immediate offset, which lets the compiler merge neighbouring
+// taps into s_buffer_load_dwordx2/x4/x8 and wait for the whole batch once.
+template <class TapT>
+__device__ __forceinline__ TapBuf tap_window(const void* taps, uint32_t T, uint32_t base) {
+  const uint64_t a = reinterpret_cast<uint64_t>(reinterpret_cast<const TapT*>(taps) + base);
+  const uint32_t bytes = base < T ? (T - base) * (uint32_t)sizeof(TapT) : 0u;
   TapBuf b;
   b.rsrc = gsdr_v4i32{(int)(uint32_t)a, (int)(uint32_t)(a >> 32) & 0xffff, (int)bytes, 0x00020000};
   return b;
 }
 
+// Tap `i` (a compile-time constant after unrolling) of a window; past T it reads as zero.
 template <class TapT>
-__device__ __forceinline__ TapT tap_at(const TapBuf& tb, uint32_t idx);
+__device__ __forceinline__ TapT tap_at(const TapBuf& tb, int i);
 template <>
-__device__ __forceinline__ float tap_at<float>(const TapBuf& tb, uint32_t idx) {
-  return gsdr_s_buffer_load_f32(tb.rsrc, (int)(idx * 4u), 0);
+__device__ __forceinline__ float tap_at<float>(const TapBuf& tb, int i) {
+  return gsdr_s_buffer_load_f32(tb.rsrc, i * 4, 0);
 }
 template <>
-__device__ __forceinline__ float2 tap_at<float2>(const TapBuf& tb, uint32_t idx) {
-  return make_float2(gsdr_s_buffer_load_f32(tb.rsrc, (int)(idx * 8u), 0),
-                     gsdr_s_buffer_load_f32(tb.rsrc, (int)(idx * 8u + 4u), 0));
+__device__ __forceinline__ float2 tap_at<float2>(const TapBuf& tb, int i) {
+  return make_float2(gsdr_s_buffer_load_f32(tb.rsrc, i * 8, 0), gsdr_s_buffer_load_f32(tb.rsrc, i * 8 + 4, 0));
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -159,6 +164,13 @@ struct TileGeo {
   __host__ __device__ static constexpr uint32_t padded(uint32_t g) { return g + PAD * (g / SG); }
 };
 
+// Non-temporal (streaming) 16-byte load: global_load_dwordx4 ... nt.
+typedef float gsdr_f32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 load16_nt(const float4* p) {
+  const gsdr_f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const gsdr_f32x4*>(p));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+
 // 16 bytes = G consecutive samples starting at s; samples at or past L read as zero.
 template <class InT, bool VEC>
 __device__ __forceinline__ float4 load_granule(const InT* __restrict__ in, uint64_t s, uint64_t L) {
@@ -188,11 +200,12 @@ __device__ __forceinline__ float4 load_granule(const InT* __restrict__ in, uint6
   return r;
 }
 
+// s = local sample index (only its low 32 bits matter: the NCO phase is taken mod 2^32).
 template <class InT, int MODE>
-__device__ __forceinline__ float4 stage_transform(float4 v, uint64_t s, const FirParams& p) {
+__device__ __forceinline__ float4 stage_transform(float4 v, uint32_t s, const FirParams& p) {
   if constexpr (MODE != kModeFir) {
     static_assert(SampleT<InT>::kPerGranule == 2, "NCO modes take complex input");
-    const uint32_t n = p.nco_n0 + (uint32_t)s;  // absolute sample index mod 2^32
+    const uint32_t n = p.nco_n0 + s;  // absolute sample index mod 2^32
     const float2 a = nco_mix(make_float2(v.x, v.y), n * p.nco_inc);
     const float2 b = nco_mix(make_float2(v.z, v.w), (n + 1u) * p.nco_inc);
     v = make_float4(a.x, a.y, b.x, b.y);
@@ -203,7 +216,7 @@ __device__ __forceinline__ float4 stage_transform(float4 v, uint64_t s, const Fi
 // Stage granules [0, NG) of the tile starting at global sample S0 into LDS (padded layout).
 // The first SG*WG granules (the tile body) are loaded fully unrolled so every HBM load is in flight
 // before the first LDS write; the remaining halo granules follow in a short strided loop.
-template <class InT, class Geo, int WG, bool VEC, int MODE>
+template <class InT, class Geo, int WG, bool VEC, int MODE, bool NT = false>
 __device__ __forceinline__ void stage_tile(float4* __restrict__ lds, const InT* __restrict__ in, uint64_t S0,
                                            uint32_t NG, const FirParams& p) {
   constexpr int G = Geo::G;
@@ -219,7 +232,13 @@ __device__ __forceinline__ void stage_tile(float4* __restrict__ lds, const InT* 
     if (whole) {
       const float4* __restrict__ src = reinterpret_cast<const float4*>(in + S0);
 #pragma unroll
-      for (int k = 0; k < SB; ++k) v[k] = src[(b0 + k) * WG + tid];
+      for (int k = 0; k < SB; ++k) {
+        if constexpr (NT) {
+          v[k] = load16_nt(src + (b0 + k) * WG + tid);
+        } else {
+          v[k] = src[(b0 + k) * WG + tid];
+        }
+      }
     } else {
 #pragma unroll
       for (int k = 0; k < SB; ++k) {
@@ -229,12 +248,12 @@ __device__ __forceinline__ void stage_tile(float4* __restrict__ lds, const InT* 
 #pragma unroll
     for (int k = 0; k < SB; ++k) {
       const uint32_t g = (b0 + k) * WG + tid;
-      lds[Geo::padded(g)] = stage_transform<InT, MODE>(v[k], S0 + (uint64_t)g * G, p);
+      lds[Geo::padded(g)] = stage_transform<InT, MODE>(v[k], (uint32_t)S0 + g * G, p);
     }
   }
   for (uint32_t g = Geo::SG * WG + tid; g < NG; g += WG) {
     const uint64_t s = S0 + (uint64_t)g * G;
-    lds[Geo::padded(g)] = stage_transform<InT, MODE>(load_granule<InT, VEC>(in, s, p.L), s, p);
+    lds[Geo::padded(g)] = stage_transform<InT, MODE>(load_granule<InT, VEC>(in, s, p.L), (uint32_t)s, p);
   }
 }
 
@@ -315,67 +334,186 @@ __device__ __forceinline__ void tile_epilogue(const FirParams& p, uint64_t out0,
 }
 
 // ------------------------------------------------------------------------------------------------
-// Kernel 1: polyphase-granule kernel, D a multiple of the granule width G.
-//   JC = tap rows per chunk (a multiple of R); a chunk covers JC*D taps.
+// Polyphase compute core shared by the polyphase kernels: thread t accumulates its R outputs from
+// the staged tile in LDS. JC = tap rows per chunk (a multiple of R); a chunk covers JC*D taps.
 // ------------------------------------------------------------------------------------------------
-// ABL (ablation, tuning probes only): 0 = full kernel, 1 = staging only, 2 = compute only.
-template <class TapT, class InT, int D, int R, int JC, int WG, bool VEC, int MODE, int ABL = 0>
-__global__ __launch_bounds__(WG) void k_fir_poly(FirParams p) {
+template <class TapT, class InT, int D, int R, int JC, int WG>
+__device__ __forceinline__ void poly_compute(const float4* __restrict__ lds, const FirParams& p,
+                                             typename Product<TapT, InT>::type (&acc)[R]) {
   using Geo = TileGeo<InT, D, R, WG>;
-  using OutT = typename Product<TapT, InT>::type;
   constexpr int G = Geo::G;
   constexpr int CPR = D / G;  // granule columns per input row
   static_assert(D % G == 0, "polyphase kernel needs whole granules per row");
   static_assert(JC % R == 0, "chunk rows must be whole thread segments");
   constexpr int NWIN = R + JC - 1;
-
-  extern __shared__ __attribute__((aligned(16))) float4 lds[];
-  const InT* __restrict__ in = reinterpret_cast<const InT*>(p.in);
-  const TapBuf taps = make_tapbuf(p.taps, p.T * (uint32_t)sizeof(TapT));
-
-  const uint64_t out0 = (uint64_t)blockIdx.x * p.tile_stride;
-  const uint64_t S0 = out0 * D;
-  const uint32_t span = p.nch * JC * D;
-  const uint32_t NG = ((Geo::KT - 1) * D + span + G - 1) / G;
-
-  if constexpr (ABL != 2) stage_tile<InT, Geo, WG, VEC, MODE>(lds, in, S0, NG, p);
-  __syncthreads();
-
-  OutT acc[R];
-#pragma unroll
-  for (int r = 0; r < R; ++r) set_zero(acc[r]);
-
   const uint32_t t = threadIdx.x;
-  if constexpr (ABL == 1) {
-    const float4 v = lds[Geo::padded(t * Geo::SG)];
-#pragma unroll
-    for (int r = 0; r < R; ++r) mac(acc[r], granule_sample<InT>(v, r % G), 1.0f);
-  }
-  for (uint32_t c = 0; c < (ABL == 1 ? 0u : p.nch); ++c) {
+  for (uint32_t c = 0; c < p.nch; ++c) {
     const float4* __restrict__ seg = lds + (t + c * (JC / R)) * Geo::SGP;
 #pragma unroll
     for (int h = 0; h < CPR; ++h) {
+      // taps first (one SMEM batch, one wait), then the LDS window (in-order, counted waits)
+      const TapBuf tb = tap_window<TapT>(p.taps, p.T, c * JC * D + h * G);
+      TapT tv[JC][G];
+#pragma unroll
+      for (int j = 0; j < JC; ++j) {
+#pragma unroll
+        for (int e = 0; e < G; ++e) tv[j][e] = tap_at<TapT>(tb, j * D + e);
+      }
       float4 win[NWIN];
 #pragma unroll
       for (int u = 0; u < NWIN; ++u) {
         const int q = u * CPR + h;
         win[u] = seg[q + Geo::PAD * (q / Geo::SG)];
       }
-      const uint32_t tap0 = c * JC * D + h * G;
 #pragma unroll
       for (int j = 0; j < JC; ++j) {
 #pragma unroll
         for (int e = 0; e < G; ++e) {
-          const TapT tv = tap_at<TapT>(taps, tap0 + j * D + e);
 #pragma unroll
-          for (int r = 0; r < R; ++r) mac(acc[r], granule_sample<InT>(win[r + j], e), tv);
+          for (int r = 0; r < R; ++r) mac(acc[r], granule_sample<InT>(win[r + j], e), tv[j][e]);
         }
       }
     }
   }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Kernel 1: polyphase-granule kernel, one tile per workgroup (D a multiple of the granule width G).
+// ABL (ablation, tuning probes only): 0 = full kernel, 1 = staging only, 2 = compute only.
+// NT: non-temporal (streaming) HBM loads for the staged input.
+// ------------------------------------------------------------------------------------------------
+template <class TapT, class InT, int D, int R, int JC, int WG, bool VEC, int MODE, int ABL = 0, bool NT = false>
+__global__ __launch_bounds__(WG) void k_fir_poly(FirParams p) {
+  using Geo = TileGeo<InT, D, R, WG>;
+  using OutT = typename Product<TapT, InT>::type;
+  constexpr int G = Geo::G;
+
+  extern __shared__ __attribute__((aligned(16))) float4 lds[];
+  const InT* __restrict__ in = reinterpret_cast<const InT*>(p.in);
+
+  const uint64_t out0 = (uint64_t)blockIdx.x * p.tile_stride;
+  const uint64_t S0 = out0 * D;
+  const uint32_t span = p.nch * JC * D;
+  const uint32_t NG = ((Geo::KT - 1) * D + span + G - 1) / G;
+
+  if constexpr (ABL != 2) stage_tile<InT, Geo, WG, VEC, MODE, NT>(lds, in, S0, NG, p);
+  __syncthreads();
+
+  OutT acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) set_zero(acc[r]);
+  if constexpr (ABL == 1) {
+    const float4 v = lds[Geo::padded(threadIdx.x * Geo::SG)];
+#pragma unroll
+    for (int r = 0; r < R; ++r) mac(acc[r], granule_sample<InT>(v, r % G), 1.0f);
+  } else {
+    poly_compute<TapT, InT, D, R, JC, WG>(lds, p, acc);
+  }
 
   float2* xs = reinterpret_cast<float2*>(lds + Geo::padded(NG - 1) + 1);
   tile_epilogue<MODE, OutT, R, WG>(p, out0, acc, xs);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Kernel 1p: the polyphase kernel as a persistent, software-pipelined loop. Each workgroup walks
+// tiles blockIdx.x, blockIdx.x + gridDim.x, ...; while it computes tile i out of LDS, the HBM loads
+// of tile i+1 are already in flight into registers (non-temporal: the input is read exactly once),
+// so every workgroup overlaps its own streaming with its own FMAs and the CU keeps 4 such
+// workgroups (16 waves) resident. HALO = granules per thread reserved for the tile's halo
+// (span - D samples past the tile body); the host only selects this kernel when they fit.
+// ------------------------------------------------------------------------------------------------
+template <class InT, int SG, int HALO>
+struct TileRegs {
+  float4 body[SG];
+  float4 halo[HALO];
+};
+
+// Non-temporal 16-byte buffer load: one SGPR descriptor + one VGPR offset for the whole tile
+// (flat loads would need a 64-bit address per load: +2 VGPRs each, which the pipeline cannot afford).
+typedef float gsdr_bf32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 buffer_load16_nt(__amdgpu_buffer_rsrc_t rsrc, uint32_t voff, uint32_t soff) {
+  const gsdr_bf32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)voff, (int)soff, 2 /* nt */);
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+
+// Issue the HBM loads of one tile into registers and return without waiting for them. The
+// descriptor's range covers only the whole granules that exist, so granules past the input's end
+// read as zero without per-granule branches; pipe_store rewrites the one granule that straddles the
+// end (odd sample count) after the fact.
+template <class InT, class Geo, int WG, int HALO>
+__device__ __forceinline__ void pipe_load(TileRegs<InT, Geo::SG, HALO>& r, const InT* __restrict__ in, uint64_t S0,
+                                          uint32_t NG, const FirParams& p) {
+  constexpr int G = Geo::G;
+  const uint32_t tid = threadIdx.x;
+  const uint64_t avail = p.L > S0 ? p.L - S0 : 0;  // samples readable from S0
+  const uint32_t nrec = avail >= (uint64_t)NG * G ? NG * 16u : (uint32_t)(avail / G) * 16u;
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(in + S0), (short)0, (int)nrec,
+                                                                       0x00020000);
+#pragma unroll
+  for (int k = 0; k < Geo::SG; ++k) r.body[k] = buffer_load16_nt(rsrc, tid * 16u, (uint32_t)(k * WG * 16));
+#pragma unroll
+  for (int k = 0; k < HALO; ++k) {
+    r.halo[k] = buffer_load16_nt(rsrc, tid * 16u, (uint32_t)((Geo::SG + k) * WG * 16));
+  }
+}
+
+template <class InT, class Geo, int WG, int HALO, int MODE>
+__device__ __forceinline__ void pipe_store(float4* __restrict__ lds, const TileRegs<InT, Geo::SG, HALO>& r,
+                                           const InT* __restrict__ in, uint64_t S0, uint32_t NG, const FirParams& p) {
+  constexpr int G = Geo::G;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t s0 = (uint32_t)S0;
+#pragma unroll
+  for (int k = 0; k < Geo::SG; ++k) {
+    const uint32_t g = k * WG + tid;
+    lds[Geo::padded(g)] = stage_transform<InT, MODE>(r.body[k], s0 + g * G, p);
+  }
+#pragma unroll
+  for (int k = 0; k < HALO; ++k) {
+    const uint32_t g = (Geo::SG + k) * WG + tid;
+    if (g < NG) lds[Geo::padded(g)] = stage_transform<InT, MODE>(r.halo[k], s0 + g * G, p);
+  }
+  const uint64_t avail = p.L > S0 ? p.L - S0 : 0;
+  if (avail < (uint64_t)NG * G && avail % G != 0) {  // wave-uniform: only the input's last tile
+    const uint32_t gl = (uint32_t)(avail / G);        // the straddling granule
+    if (gl % WG == tid) {
+      lds[Geo::padded(gl)] = stage_transform<InT, MODE>(load_granule<InT, false>(in, S0 + (uint64_t)gl * G, p.L),
+                                                        s0 + gl * G, p);
+    }
+  }
+}
+
+template <class TapT, class InT, int D, int R, int JC, int WG, int HALO, int MODE>
+__global__ __launch_bounds__(WG, 4) void k_fir_poly_pipe(FirParams p, uint32_t ntiles) {
+  using Geo = TileGeo<InT, D, R, WG>;
+  using OutT = typename Product<TapT, InT>::type;
+  constexpr int G = Geo::G;
+
+  extern __shared__ __attribute__((aligned(16))) float4 lds[];
+  const InT* __restrict__ in = reinterpret_cast<const InT*>(p.in);
+  const uint32_t span = p.nch * JC * D;
+  const uint32_t NG = ((Geo::KT - 1) * D + span + G - 1) / G;
+  float2* xs = reinterpret_cast<float2*>(lds + Geo::padded(NG - 1) + 1);
+
+  uint32_t tile = blockIdx.x;
+  if (tile >= ntiles) return;
+  TileRegs<InT, Geo::SG, HALO> regs;
+  pipe_load<InT, Geo, WG, HALO>(regs, in, (uint64_t)tile * p.tile_stride * D, NG, p);
+  for (;;) {
+    const uint64_t out0 = (uint64_t)tile * p.tile_stride;
+    pipe_store<InT, Geo, WG, HALO, MODE>(lds, regs, in, out0 * D, NG, p);
+    __syncthreads();
+    const uint32_t next = tile + gridDim.x;
+    if (next < ntiles) pipe_load<InT, Geo, WG, HALO>(regs, in, (uint64_t)next * p.tile_stride * D, NG, p);
+    OutT acc[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) set_zero(acc[r]);
+    poly_compute<TapT, InT, D, R, JC, WG>(lds, p, acc);
+    tile_epilogue<MODE, OutT, R, WG>(p, out0, acc, xs);
+    if (next >= ntiles) break;
+    __syncthreads();  // every wave is done reading this tile before the next one overwrites it
+    tile = next;
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -393,7 +531,6 @@ __global__ __launch_bounds__(WG) void k_fir_contig(FirParams p) {
 
   extern __shared__ __attribute__((aligned(16))) float4 lds[];
   const InT* __restrict__ in = reinterpret_cast<const InT*>(p.in);
-  const TapBuf taps = make_tapbuf(p.taps, p.T * (uint32_t)sizeof(TapT));
 
   const uint64_t out0 = (uint64_t)blockIdx.x * p.tile_stride;
   const uint64_t S0 = out0 * D;
@@ -410,12 +547,16 @@ __global__ __launch_bounds__(WG) void k_fir_contig(FirParams p) {
   const uint32_t t = threadIdx.x;
   for (uint32_t c = 0; c < p.nch; ++c) {
     const float4* __restrict__ seg = lds + (t + c * (IC / (R * D))) * Geo::SGP;
+    const TapBuf tb = tap_window<TapT>(p.taps, p.T, c * IC);
+    TapT tvs[IC];
+#pragma unroll
+    for (int i = 0; i < IC; ++i) tvs[i] = tap_at<TapT>(tb, i);
     float4 win[NWIN];
 #pragma unroll
     for (int q = 0; q < NWIN; ++q) win[q] = seg[q + Geo::PAD * (q / Geo::SG)];
 #pragma unroll
     for (int i = 0; i < IC; ++i) {
-      const TapT tv = tap_at<TapT>(taps, c * IC + i);
+      const TapT tv = tvs[i];
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         const int s = r * D + i;

@@ -22,22 +22,24 @@ ap.add_argument("--variants", default="0,1,2,3,4,5,6,100,101,102")
 ap.add_argument("--reps", type=int, default=20)
 ap.add_argument("--rounds", type=int, default=3)
 ap.add_argument("--fm", action="store_true", help="also time the fused FM chain")
+ap.add_argument("--buffers", type=int, default=3, help="input buffers rotated per launch (3 x 537 MB defeats the 256 MB MALL)")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 g = torch.Generator(device=dev).manual_seed(0x5EED)
-x = (torch.rand(2 * L, device=dev, generator=g) * 2 - 1).view(torch.complex64)
+xs = [(torch.rand(2 * L, device=dev, generator=g) * 2 - 1).view(torch.complex64) for _ in range(a.buffers)]
+x = xs[0]
 taps = torch.from_numpy(lowpass_taps(TAPS)).to(dev)
 y = torch.empty(N, dtype=torch.complex64, device=dev)
 variants = [int(v) for v in a.variants.split(",")]
 res = {v: [] for v in variants}
 for r in range(a.rounds):
     for v in variants:
-        for _ in range(2):
-            ops.fir_variant(v, taps, x, D, N, out=y)
+        for i in range(2):
+            ops.fir_variant(v, taps, xs[i % len(xs)], D, N, out=y)
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
-        for _ in range(a.reps):
-            ops.fir_variant(v, taps, x, D, N, out=y)
+        for i in range(a.reps):
+            ops.fir_variant(v, taps, xs[i % len(xs)], D, N, out=y)
         e.record()
         torch.cuda.synchronize()
         res[v].append(s.elapsed_time(e) / a.reps * 1e3)

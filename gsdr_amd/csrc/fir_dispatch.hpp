@@ -193,6 +193,14 @@ hipError_t launch_d4_complex(const FirJob& j, hipStream_t s) {
       return launch_poly_pipe<TapT, InT, 4, 4, 16, 128, 1, MODE>(j, s);
     case 23:
       return launch_poly_pipe<TapT, InT, 4, 4, 16, 256, 1, MODE>(j, s, 2);
+    case 24:  // single-wave workgroups: wave-local barriers, waves drift apart freely
+      return launch_poly<TapT, InT, 4, 4, 16, 64, MODE>(j, s);
+    case 25:
+      return launch_poly_pipe<TapT, InT, 4, 4, 16, 64, 1, MODE>(j, s);
+    case 26:
+      return launch_poly_pipe<TapT, InT, 4, 4, 8, 64, 1, MODE>(j, s);
+    case 27:
+      return launch_poly<TapT, InT, 4, 8, 16, 64, MODE>(j, s);
     default:
       return launch_poly<TapT, InT, 4, 4, 16, 256, MODE>(j, s);
   }

@@ -1,0 +1,78 @@
+"""CPU, world_size 2 over gloo: the multi-GPU path of bench.py (independent channels, one per rank,
+no data-path collective; barrier + max-over-ranks timing; whole-job aggregate). Each rank filters
+its own channel with the CPU oracle standing in for the device (no GPU here) and the test checks
+the bookkeeping, not the FIR: channels differ by seed, the reduced time is the slowest rank's, and
+value = world x per-rank samples / max time (weak scaling)."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import bench
+    from gsdr_amd.signals import lowpass_taps, uniform_iq
+    from oracle import oracle as orc
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        assert bench.dist_env() == (rank, rank, world)
+        seed = bench.channel_seed(rank)
+        n_out, D, T = 4096, 4, 127
+        x = uniform_iq((n_out - 1) * D + T, seed=seed)
+        y = orc.fir(lowpass_taps(T), x, D, n_out)
+        local_time = 0.010 * (rank + 1)  # rank 1 is the slow one
+        bench.barrier()
+        tmax = bench.reduce_max(local_time, torch.device("cpu"))
+        digest = torch.tensor([float(np.abs(y).sum())])
+        gathered = [torch.zeros(1) for _ in range(world)]
+        dist.all_gather(gathered, digest)  # test-side only: compare the channels the ranks produced
+        q.put((rank, seed, tmax, [float(g) for g in gathered]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+def test_two_rank_channels_and_timing():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = sorted(q.get(timeout=150) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    seeds = [r[1] for r in results]
+    assert seeds == [0x5EED, 0x5EED + 1]  # one independent channel per rank
+    assert all(abs(r[2] - 0.020) < 1e-12 for r in results)  # every rank sees the slowest rank's time
+    digests = results[0][3]
+    assert digests == results[1][3] and digests[0] != digests[1]  # channels really differ
+
+
+def test_aggregate_is_weak_scaling():
+    sys.path.insert(0, ROOT)
+    import bench
+
+    one = bench.aggregate(bench.N_IN, 1, 10, 1.0e-3)
+    eight = bench.aggregate(bench.N_IN, 8, 10, 1.0e-3)
+    assert eight == pytest.approx(8 * one)
+    assert one == pytest.approx(bench.N_IN * 10 / 1.0e-3 / 1e6)

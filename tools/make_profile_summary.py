@@ -1,0 +1,44 @@
+#!/usr/bin/env python3
+"""Copy the round's rocprofv3 evidence into profiles/ (tracked):
+  profiles/<tag>_bench_kernel_stats.csv   rocprofv3 --kernel-trace --stats of `python bench.py`
+  profiles/<tag>_pmc_summary.json         per-kernel PMC means (tools/pmc_summary.py)
+  profiles/pmc_fir_fc_d4.json             HBM bytes per launch of the headline kernel, read by bench.py
+usage: tools/make_profile_summary.py <tag> [--kernel substr]
+"""
+import argparse
+import glob
+import json
+import os
+import shutil
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ap = argparse.ArgumentParser()
+ap.add_argument("tag")
+ap.add_argument("--kernel", default="void k_fir_poly<float, f2, 4, 4, 16, 256, true, 0, 0, false>")
+ap.add_argument("--stats-dir", default="gpurun_out/prof_bench")
+ap.add_argument("--pmc-dir", default="gpurun_out/pmc_bench")
+a = ap.parse_args()
+prof = os.path.join(ROOT, "profiles")
+os.makedirs(prof, exist_ok=True)
+stats = glob.glob(os.path.join(ROOT, a.stats_dir, "**", "*kernel_stats.csv"), recursive=True)
+if stats:
+    shutil.copy(stats[0], os.path.join(prof, f"{a.tag}_bench_kernel_stats.csv"))
+summ = json.load(open(os.path.join(ROOT, a.pmc_dir, "summary.json")))
+shutil.copy(os.path.join(ROOT, a.pmc_dir, "summary.json"), os.path.join(prof, f"{a.tag}_pmc_summary.json"))
+k = summ[a.kernel]
+out = {
+    "kernel": a.kernel,
+    "hbm_bytes_per_launch": round(k["hbm_bytes_corrected"]),
+    "fetch_size_kib": k["FETCH_SIZE"],
+    "write_size_kib": k["WRITE_SIZE"],
+    "correction": "hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024: on gfx950 FETCH_SIZE reports half the bytes "
+                  "of a wide coalesced stream, WRITE_SIZE is exact (MI355X_MICROARCH.md, HBM section)",
+    "pmc_duration_us_mean": k.get("duration_us_mean"),
+    "command": "tools/pmc.sh pmc_bench python bench.py --steps 3 --warmup 1 --no-secondary --no-cpu-baseline "
+               "(one rocprofv3 --pmc pass per counter group)",
+    "round": a.tag,
+    "generated": time.strftime("%Y-%m-%d %H:%M:%S"),
+}
+json.dump(out, open(os.path.join(prof, "pmc_fir_fc_d4.json"), "w"), indent=1)
+print(json.dumps(out, indent=1))

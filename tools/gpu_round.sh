@@ -10,6 +10,7 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 rc=$?; echo "smoke exit $rc"; tail -1 gpurun_out/smoke.log; ok $rc || exit $rc
 timeout -k 10 600 python bench.py > gpurun_out/bench.log 2>&1
 rc=$?; echo "bench exit $rc"; tail -1 gpurun_out/bench.log; [ $rc = 0 ] || exit $rc
+rm -rf gpurun_out/prof_bench gpurun_out/pmc_bench
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench -- python bench.py > gpurun_out/prof_bench.log 2>&1
 rc=$?; echo "rocprof bench exit $rc"; [ $rc = 0 ] || exit $rc
 bash tools/pmc.sh pmc_bench python bench.py --steps 3 --warmup 1 --no-secondary --no-cpu-baseline > gpurun_out/pmc_bench.log 2>&1

@@ -18,12 +18,26 @@ ap.add_argument("tag")
 ap.add_argument("--kernel", default="void k_fir_poly<float, f2, 4, 4, 16, 256, true, 0, 0, false>")
 ap.add_argument("--stats-dir", default="gpurun_out/prof_bench")
 ap.add_argument("--pmc-dir", default="gpurun_out/pmc_bench")
+ap.add_argument("--steps", type=int, default=100, help="timed steps of the profiled bench run")
 a = ap.parse_args()
 prof = os.path.join(ROOT, "profiles")
 os.makedirs(prof, exist_ok=True)
-stats = glob.glob(os.path.join(ROOT, a.stats_dir, "**", "*kernel_stats.csv"), recursive=True)
+stats = sorted(glob.glob(os.path.join(ROOT, a.stats_dir, "**", "*kernel_stats.csv"), recursive=True),
+               key=os.path.getmtime)
+timed_mean = None
 if stats:
-    shutil.copy(stats[0], os.path.join(prof, f"{a.tag}_bench_kernel_stats.csv"))
+    shutil.copy(stats[-1], os.path.join(prof, f"{a.tag}_bench_kernel_stats.csv"))
+    trace = stats[-1].replace("kernel_stats.csv", "kernel_trace.csv")
+    import csv
+    fir_name = "void gsdr::" + a.kernel[len("void "):].replace("f2", "HIP_vector_type<float, 2u>")
+    d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3 for r in csv.DictReader(open(trace))
+         if r["Kernel_Name"].startswith(fir_name)]
+    if d:
+        timed_mean = sum(d[-a.steps:]) / len(d[-a.steps:])
+        with open(os.path.join(prof, f"{a.tag}_bench_fir_dispatches.txt"), "w") as f:
+            f.write(f"# {fir_name}: per-dispatch duration (us) from rocprofv3 --kernel-trace of `python bench.py`\n")
+            f.write(f"# dispatches {len(d)}; mean of the last {a.steps} (the timed steps) = {timed_mean:.2f} us\n")
+            f.write("\n".join(f"{x:.2f}" for x in d) + "\n")
 summ = json.load(open(os.path.join(ROOT, a.pmc_dir, "summary.json")))
 shutil.copy(os.path.join(ROOT, a.pmc_dir, "summary.json"), os.path.join(prof, f"{a.tag}_pmc_summary.json"))
 k = summ[a.kernel]
@@ -35,6 +49,7 @@ out = {
     "correction": "hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024: on gfx950 FETCH_SIZE reports half the bytes "
                   "of a wide coalesced stream, WRITE_SIZE is exact (MI355X_MICROARCH.md, HBM section)",
     "pmc_duration_us_mean": k.get("duration_us_mean"),
+    "rocprof_timed_steps_us_mean": timed_mean,
     "command": "tools/pmc.sh pmc_bench python bench.py --steps 3 --warmup 1 --no-secondary --no-cpu-baseline "
                "(one rocprofv3 --pmc pass per counter group)",
     "round": a.tag,

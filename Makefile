@@ -31,7 +31,14 @@ oracle/build/liboracle.so: oracle/gsdr_oracle.c oracle/gsdr_oracle.h
 	@mkdir -p oracle/build
 	$(CC) $(OFLAGS) -shared oracle/gsdr_oracle.c -o $@ -lm -lpthread
 
+# C++ host example linking the C ABI
+examples: $(BUILD)/fm_receiver
+
+$(BUILD)/fm_receiver: examples/fm_receiver.cpp gsdr_amd/libgsdr.so $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) -O2 -std=c++17 -Iinclude $< -Lgsdr_amd -lgsdr -Wl,-rpath,'$$ORIGIN/../gsdr_amd' -o $@
+
 clean:
 	rm -rf $(BUILD) gsdr_amd/libgsdr.so oracle/build
 
-.PHONY: all clean
+.PHONY: all clean examples

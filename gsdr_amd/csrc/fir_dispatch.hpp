@@ -61,7 +61,8 @@ hipError_t launch_generic(const FirJob& j, hipStream_t s) {
   return launch_status();
 }
 
-template <class TapT, class InT, int D, int R, int JC, int WG, int MODE, int ABL = 0, bool NT = false>
+template <class TapT, class InT, int D, int R, int JC, int WG, int MODE, int ABL = 0, bool NT = false,
+          bool TL = false>
 hipError_t launch_poly(const FirJob& j, hipStream_t s) {
   using Geo = TileGeo<InT, D, R, WG>;
   FirParams p = make_params(j);
@@ -69,7 +70,7 @@ hipError_t launch_poly(const FirJob& j, hipStream_t s) {
   const uint64_t nch = ceil_div<uint64_t>(rows, (uint64_t)JC);
   const uint64_t span = nch * JC * D;
   if (span > 0x40000000ull) return launch_generic<TapT, InT, MODE>(j, s);
-  const size_t lds = poly_lds_bytes<InT, D, R, WG>((uint32_t)span, MODE);
+  const size_t lds = poly_lds_bytes<InT, D, R, WG>((uint32_t)span, MODE, TL ? span * sizeof(TapT) : 0);
   if (lds > kMaxTileLds) return launch_generic<TapT, InT, MODE>(j, s);
   p.nch = (uint32_t)nch;
   const uint32_t stride = (MODE == kModeFm) ? Geo::KT - 1 : Geo::KT;
@@ -78,9 +79,9 @@ hipError_t launch_poly(const FirJob& j, hipStream_t s) {
   if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
   const bool vec = aligned16(j.in) && ((uint64_t)stride * D * sizeof(InT)) % 16 == 0;
   if (vec) {
-    k_fir_poly<TapT, InT, D, R, JC, WG, true, MODE, ABL, NT><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
+    k_fir_poly<TapT, InT, D, R, JC, WG, true, MODE, ABL, NT, TL><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
   } else {
-    k_fir_poly<TapT, InT, D, R, JC, WG, false, MODE, ABL, NT><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
+    k_fir_poly<TapT, InT, D, R, JC, WG, false, MODE, ABL, NT, TL><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
   }
   return launch_status();
 }
@@ -158,6 +159,66 @@ hipError_t launch_poly_pipe(const FirJob& j, hipStream_t s, int oversubscribe = 
   return launch_status();
 }
 
+// Persistent LDS-DMA pipeline (k_fir_poly_dma), FIR mode, 16-byte aligned input only; otherwise the
+// one-tile kernel.
+template <class TapT, class InT, int D, int R, int JC, int WG, bool TL = false>
+hipError_t launch_poly_dma(const FirJob& j, hipStream_t s) {
+  using Geo = TileGeo<InT, D, R, WG>;
+  FirParams p = make_params(j);
+  const uint64_t rows = ceil_div<uint64_t>(j.T, (uint64_t)D);
+  const uint64_t nch = ceil_div<uint64_t>(rows, (uint64_t)JC);
+  const uint64_t span = nch * JC * D;
+  const uint64_t stride = Geo::KT;
+  const bool vec = aligned16(j.in) && (stride * D * sizeof(InT)) % 16 == 0;
+  if (!vec || span > (1u << 20)) return launch_poly<TapT, InT, D, R, JC, WG, kModeFir>(j, s);
+  const uint64_t NG = ((uint64_t)(Geo::KT - 1) * D + span + Geo::G - 1) / Geo::G;
+  const uint64_t NGP = Geo::padded((uint32_t)(NG - 1)) + 1;
+  const uint32_t slots = (uint32_t)ceil_div<uint64_t>(NGP, WG) * WG;
+  const size_t lds = 2ull * slots * 16u + (TL ? span * sizeof(TapT) : 0);
+  if (lds > 160 * 1024) return launch_poly<TapT, InT, D, R, JC, WG, kModeFir>(j, s);
+  p.nch = (uint32_t)nch;
+  p.tile_stride = (uint32_t)stride;
+  const uint64_t tiles = ceil_div<uint64_t>(j.N, stride);
+  if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
+  const void* kern = reinterpret_cast<const void*>(&k_fir_poly_dma<TapT, InT, D, R, JC, WG, TL>);
+  if (lds > 64 * 1024) {
+    const hipError_t st = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (st != hipSuccess) return st;
+  }
+  uint32_t grid = persistent_grid(kern, WG, lds, 1);
+  if (grid == 0) return hipErrorInvalidDevice;
+  if (grid > tiles) grid = (uint32_t)tiles;
+  k_fir_poly_dma<TapT, InT, D, R, JC, WG, TL><<<dim3(grid), dim3(WG), lds, s>>>(p, (uint32_t)tiles, slots);
+  return launch_status();
+}
+
+// Column-split polyphase kernel (k_fir_poly_cs): D = 2 granules per row, FIR mode, NCH compile-time
+// chunk count (taps held in SGPRs for the whole kernel).
+template <class TapT, class InT, int D, int R, int JC, int WG, int NCH, bool NT = false>
+hipError_t launch_poly_cs(const FirJob& j, hipStream_t s) {
+  using Geo = TileGeo<InT, D, R, WG / 2>;
+  using OutT = typename Product<TapT, InT>::type;
+  FirParams p = make_params(j);
+  const uint64_t rows = ceil_div<uint64_t>(j.T, (uint64_t)D);
+  const uint64_t nch = ceil_div<uint64_t>(rows, (uint64_t)JC);
+  if (nch > (uint64_t)NCH) return launch_poly<TapT, InT, D, R, JC, WG, kModeFir>(j, s);
+  p.nch = NCH;  // fewer real chunks read zero taps (range-checked) -- same result
+  const uint32_t span = NCH * JC * D;
+  const uint32_t NG = ((Geo::KT - 1) * D + span + Geo::G - 1) / Geo::G;
+  const size_t lds = (size_t)(Geo::padded(NG - 1) + 1) * 16u + (size_t)(WG / 2) * R * sizeof(OutT);
+  if (lds > kMaxTileLds) return launch_generic<TapT, InT, kModeFir>(j, s);
+  p.tile_stride = Geo::KT;
+  const uint64_t tiles = ceil_div<uint64_t>(j.N, (uint64_t)Geo::KT);
+  if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
+  const bool vec = aligned16(j.in) && ((uint64_t)Geo::KT * D * sizeof(InT)) % 16 == 0;
+  if (vec) {
+    k_fir_poly_cs<TapT, InT, D, R, JC, WG, NCH, true, NT><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
+  } else {
+    k_fir_poly_cs<TapT, InT, D, R, JC, WG, NCH, false, NT><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
+  }
+  return launch_status();
+}
+
 // Tile-shape variants of the headline case (real taps, complex input, D = 4), selectable through
 // gsdrxFirFCVariant for tuning sweeps. Variant 0 is the default (WG = 256, R = 4, JC = 16);
 // variant 1 is the round-1 starting shape (WG = 128, R = 8).
@@ -201,6 +262,48 @@ hipError_t launch_d4_complex(const FirJob& j, hipStream_t s) {
       return launch_poly_pipe<TapT, InT, 4, 4, 8, 64, 1, MODE>(j, s);
     case 27:
       return launch_poly<TapT, InT, 4, 8, 16, 64, MODE>(j, s);
+    case 30:  // LDS-DMA double-buffered pipeline: 2 x 38 KB per WG -> 2 WGs (8 waves) per CU
+      return launch_poly_dma<TapT, InT, 4, 4, 16, 256>(j, s);
+    case 31:  // R = 2: 2 x 25 KB -> 3 WGs (12 waves) per CU
+      return launch_poly_dma<TapT, InT, 4, 2, 16, 256>(j, s);
+    case 32:  // WG = 512, R = 2: 8 waves in one WG per CU
+      return launch_poly_dma<TapT, InT, 4, 2, 16, 512>(j, s);
+    case 33:  // WG = 128, R = 4: 2 x 20 KB -> 3 WGs per CU
+      return launch_poly_dma<TapT, InT, 4, 4, 16, 128>(j, s);
+    case 40:  // default shape, taps staged in LDS
+      return launch_poly<TapT, InT, 4, 4, 16, 256, MODE, 0, false, true>(j, s);
+    case 41:  // R = 8, WG = 128, taps in LDS
+      return launch_poly<TapT, InT, 4, 8, 16, 128, MODE, 0, false, true>(j, s);
+    case 42:  // DMA pipeline, taps in LDS
+      return launch_poly_dma<TapT, InT, 4, 4, 16, 256, true>(j, s);
+    case 43:
+      return launch_poly_dma<TapT, InT, 4, 4, 16, 128, true>(j, s);
+    case 44:  // R = 4, WG = 256, JC = 32, taps in LDS
+      return launch_poly<TapT, InT, 4, 4, 32, 256, MODE, 0, false, true>(j, s);
+    case 45:
+      return launch_poly<TapT, InT, 4, 4, 8, 256, MODE, 0, false, true>(j, s);
+    case 46:
+      return launch_poly<TapT, InT, 4, 8, 8, 128, MODE, 0, false, true>(j, s);
+    case 47:
+      return launch_poly<TapT, InT, 4, 8, 8, 64, MODE, 0, false, true>(j, s);
+    case 50:  // column split, R = 8, 2 pairs of waves, taps in SGPRs once
+      return launch_poly_cs<TapT, InT, 4, 8, 16, 256, 2>(j, s);
+    case 51:
+      return launch_poly_cs<TapT, InT, 4, 4, 16, 256, 2>(j, s);
+    case 52:
+      return launch_poly_cs<TapT, InT, 4, 8, 16, 128, 2>(j, s);
+    case 53:
+      return launch_poly_cs<TapT, InT, 4, 4, 16, 512, 2>(j, s);
+    case 54:  // column split R = 8 with non-temporal loads and stores
+      return launch_poly_cs<TapT, InT, 4, 8, 16, 256, 2, true>(j, s);
+    case 55:  // default shape with non-temporal loads and stores
+      return launch_poly<TapT, InT, 4, 4, 16, 256, MODE, 0, true>(j, s);
+    case 56:
+      return launch_poly_cs<TapT, InT, 4, 4, 16, 256, 2, true>(j, s);
+    case 48:
+      return launch_poly_dma<TapT, InT, 4, 4, 8, 256, true>(j, s);
+    case 49:
+      return launch_poly_dma<TapT, InT, 4, 8, 8, 128, true>(j, s);
     default:
       return launch_poly<TapT, InT, 4, 4, 16, 256, MODE>(j, s);
   }
@@ -216,15 +319,15 @@ hipError_t launch_fir(const FirJob& j, hipStream_t s) {
       case 1:
         return launch_contig<TapT, InT, 1, 8, 16, 256, MODE>(j, s);
       case 2:
-        return launch_poly<TapT, InT, 2, 8, 16, 128, MODE>(j, s);
+        return launch_poly<TapT, InT, 2, 8, 16, 128, MODE, 0, true>(j, s);
       case 4:
         if constexpr (MODE == kModeFir && std::is_same<TapT, float>::value) {
           if (j.variant >= 0) return launch_d4_complex<TapT, InT, MODE>(j, s);
         }
         // 4 waves/SIMD (16 per CU): the shape that measured fastest at T = 127
-        return launch_poly<TapT, InT, 4, 4, 16, 256, MODE>(j, s);
+        return launch_poly<TapT, InT, 4, 4, 16, 256, MODE, 0, true>(j, s);
       case 8:
-        return launch_poly<TapT, InT, 8, 8, 8, 128, MODE>(j, s);
+        return launch_poly<TapT, InT, 8, 8, 8, 128, MODE, 0, true>(j, s);
       default:
         return launch_generic<TapT, InT, MODE>(j, s);
     }
@@ -235,9 +338,9 @@ hipError_t launch_fir(const FirJob& j, hipStream_t s) {
       case 2:
         return launch_contig<TapT, InT, 2, 8, 16, 256, MODE>(j, s);
       case 4:
-        return launch_poly<TapT, InT, 4, 8, 8, 128, MODE>(j, s);
+        return launch_poly<TapT, InT, 4, 8, 8, 128, MODE, 0, true>(j, s);
       case 8:
-        return launch_poly<TapT, InT, 8, 8, 8, 128, MODE>(j, s);
+        return launch_poly<TapT, InT, 8, 8, 8, 128, MODE, 0, true>(j, s);
       default:
         return launch_generic<TapT, InT, MODE>(j, s);
     }

@@ -141,14 +141,35 @@ struct FirParams {
 };
 
 // ------------------------------------------------------------------------------------------------
-// NCO: exact integer phase, float sincospi.
+// NCO: exact integer phase P(n) = n * inc mod 2^32 from the absolute sample
+// index n, turned into a unit phasor by a fixed function of n alone, so any split of a stream into
+// calls (and any tiling inside a call) mixes every sample with bit-identical values:
+//   n even: (cos, sin)(2 pi P(n) / 2^32) from the hardware v_cos_f32 / v_sin_f32, whose argument is
+//           in revolutions (max abs error 1.9e-7 measured over 2^28 phases, tools/nco_accuracy.hip;
+//           the (int32)P -> float rounding adds <= 2^-25 revolutions, as sincospif did);
+//   n odd:  phasor(n - 1) rotated by w = phasor of one step (P = inc).
+// One transcendental pair per two samples: the mixer was a third of the FM chain's VALU work with
+// a sincospif per sample.
 // ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ float2 nco_mix(float2 x, uint32_t phase) {
-  float sn, cs;
-  // phase / 2^32 cycles == (int32)phase / 2^31 half-cycles, in [-1, 1)
-  sincospif((float)(int32_t)phase * 0x1p-31f, &sn, &cs);
-  return make_float2(x.x * cs - x.y * sn, x.x * sn + x.y * cs);
+__device__ __forceinline__ float2 nco_direct(uint32_t phase) {
+  const float r = (float)(int32_t)phase * 0x1p-32f;  // revolutions in [-0.5, 0.5)
+  return make_float2(__builtin_amdgcn_cosf(r), __builtin_amdgcn_sinf(r));
 }
+
+// a * b with explicit fmas (pk_mul + pk_fma; the library builds with -ffp-contract=off, so the
+// rounding is fixed here rather than left to the contraction pass)
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+  return make_float2(fmaf(a.x, b.x, -(a.y * b.y)), fmaf(a.x, b.y, a.y * b.x));
+}
+
+// phasor of absolute sample n (low 32 bits suffice: P is taken mod 2^32)
+__device__ __forceinline__ float2 nco_phasor(uint32_t n, uint32_t inc) {
+  const float2 w = nco_direct(inc);
+  const float2 e = nco_direct((n & ~1u) * inc);
+  return (n & 1u) ? cmul(e, w) : e;
+}
+
+__device__ __forceinline__ float2 nco_mix(float2 x, uint32_t n, uint32_t inc) { return cmul(x, nco_phasor(n, inc)); }
 
 // ------------------------------------------------------------------------------------------------
 // Tile geometry
@@ -161,6 +182,7 @@ struct TileGeo {
   static constexpr int PAD = (SG % 2 == 0) ? 1 : 0;  // odd lane stride -> conflict-free ds_read_b128
   static constexpr int SGP = SG + PAD;
   static constexpr int KT = WG * R;                  // outputs per tile
+  static constexpr int ROUT = R;                     // outputs per segment
   __host__ __device__ static constexpr uint32_t padded(uint32_t g) { return g + PAD * (g / SG); }
 };
 
@@ -201,13 +223,24 @@ __device__ __forceinline__ float4 load_granule(const InT* __restrict__ in, uint6
 }
 
 // s = local sample index (only its low 32 bits matter: the NCO phase is taken mod 2^32).
+// s = local sample index of a granule's first sample (only its low 32 bits matter).
 template <class InT, int MODE>
 __device__ __forceinline__ float4 stage_transform(float4 v, uint32_t s, const FirParams& p) {
   if constexpr (MODE != kModeFir) {
     static_assert(SampleT<InT>::kPerGranule == 2, "NCO modes take complex input");
-    const uint32_t n = p.nco_n0 + s;  // absolute sample index mod 2^32
-    const float2 a = nco_mix(make_float2(v.x, v.y), n * p.nco_inc);
-    const float2 b = nco_mix(make_float2(v.z, v.w), (n + 1u) * p.nco_inc);
+    const uint32_t n = p.nco_n0 + s;  // absolute index of the granule's first sample mod 2^32
+    const float2 w = nco_direct(p.nco_inc);
+    float2 ea, eb;
+    // wave-uniform: the tiled kernels stage granules at even offsets from an even-or-odd tile start
+    if (__builtin_amdgcn_readfirstlane(n & 1u) == 0) {
+      ea = nco_direct(n * p.nco_inc);
+      eb = cmul(ea, w);
+    } else {
+      ea = cmul(nco_direct((n - 1u) * p.nco_inc), w);
+      eb = nco_direct((n + 1u) * p.nco_inc);
+    }
+    const float2 a = cmul(make_float2(v.x, v.y), ea);
+    const float2 b = cmul(make_float2(v.z, v.w), eb);
     v = make_float4(a.x, a.y, b.x, b.y);
   }
   return v;
@@ -220,14 +253,17 @@ template <class InT, class Geo, int WG, bool VEC, int MODE, bool NT = false>
 __device__ __forceinline__ void stage_tile(float4* __restrict__ lds, const InT* __restrict__ in, uint64_t S0,
                                            uint32_t NG, const FirParams& p) {
   constexpr int G = Geo::G;
+  // tile body granules per staging thread (Geo::KT / R output segments of SG granules over WG threads)
+  constexpr int BPT = Geo::SG * (Geo::KT / Geo::ROUT) / WG;
+  static_assert(BPT * WG == Geo::SG * (Geo::KT / Geo::ROUT), "tile body must split evenly over the threads");
   // at most 8 granules (128 B) in flight per lane: bounds the staging registers for large segments
-  constexpr int SB = Geo::SG < 8 ? Geo::SG : 8;
-  static_assert(Geo::SG % SB == 0, "segment granules must split into whole staging batches");
+  constexpr int SB = BPT < 8 ? BPT : 8;
+  static_assert(BPT % SB == 0, "segment granules must split into whole staging batches");
   const uint32_t tid = threadIdx.x;
   // wave-uniform: is the whole staged span readable? (every tile but the last)
   const bool whole = VEC && (S0 + (uint64_t)NG * G <= p.L);
 #pragma unroll
-  for (int b0 = 0; b0 < Geo::SG; b0 += SB) {
+  for (int b0 = 0; b0 < BPT; b0 += SB) {
     float4 v[SB];
     if (whole) {
       const float4* __restrict__ src = reinterpret_cast<const float4*>(in + S0);
@@ -251,7 +287,7 @@ __device__ __forceinline__ void stage_tile(float4* __restrict__ lds, const InT* 
       lds[Geo::padded(g)] = stage_transform<InT, MODE>(v[k], (uint32_t)S0 + g * G, p);
     }
   }
-  for (uint32_t g = Geo::SG * WG + tid; g < NG; g += WG) {
+  for (uint32_t g = BPT * WG + tid; g < NG; g += WG) {
     const uint64_t s = S0 + (uint64_t)g * G;
     lds[Geo::padded(g)] = stage_transform<InT, MODE>(load_granule<InT, VEC>(in, s, p.L), (uint32_t)s, p);
   }
@@ -260,7 +296,11 @@ __device__ __forceinline__ void stage_tile(float4* __restrict__ lds, const InT* 
 // ------------------------------------------------------------------------------------------------
 // Epilogues
 // ------------------------------------------------------------------------------------------------
-template <class OutT, int R>
+__device__ __forceinline__ void store16_nt(float4* p, float4 v) {
+  __builtin_nontemporal_store(gsdr_f32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<gsdr_f32x4*>(p));
+}
+
+template <class OutT, int R, bool NTS = false>
 __device__ __forceinline__ void store_fir(OutT* __restrict__ out, uint64_t k0, uint64_t N, const OutT (&acc)[R]) {
   constexpr int PER16 = 16 / sizeof(OutT);
   static_assert(R % PER16 == 0, "R must fill whole 16-byte stores");
@@ -278,7 +318,11 @@ __device__ __forceinline__ void store_fir(OutT* __restrict__ out, uint64_t k0, u
                         reinterpret_cast<const float&>(acc[4 * q + 2]),
                         reinterpret_cast<const float&>(acc[4 * q + 3]));
       }
-      o[q] = w;
+      if constexpr (NTS) {
+        store16_nt(o + q, w);
+      } else {
+        o[q] = w;
+      }
     }
   } else {
 #pragma unroll
@@ -304,12 +348,12 @@ __device__ __forceinline__ float am_env(float2 y) {
 }
 
 // Shared by both tiled kernels. `xs` is a WG-sized LDS exchange area (FM mode only).
-template <int MODE, class OutT, int R, int WG>
+template <int MODE, class OutT, int R, int WG, bool NTS = false>
 __device__ __forceinline__ void tile_epilogue(const FirParams& p, uint64_t out0, OutT (&acc)[R], float2* xs) {
   const uint32_t t = threadIdx.x;
   const uint32_t local0 = t * R;
   if constexpr (MODE == kModeFir) {
-    store_fir<OutT, R>(reinterpret_cast<OutT*>(p.out), out0 + local0, p.N, acc);
+    store_fir<OutT, R, NTS>(reinterpret_cast<OutT*>(p.out), out0 + local0, p.N, acc);
   } else if constexpr (MODE == kModeAm) {
     float* out = reinterpret_cast<float*>(p.out);
 #pragma unroll
@@ -337,9 +381,10 @@ __device__ __forceinline__ void tile_epilogue(const FirParams& p, uint64_t out0,
 // Polyphase compute core shared by the polyphase kernels: thread t accumulates its R outputs from
 // the staged tile in LDS. JC = tap rows per chunk (a multiple of R); a chunk covers JC*D taps.
 // ------------------------------------------------------------------------------------------------
-template <class TapT, class InT, int D, int R, int JC, int WG>
+template <class TapT, class InT, int D, int R, int JC, int WG, bool TAPS_LDS = false>
 __device__ __forceinline__ void poly_compute(const float4* __restrict__ lds, const FirParams& p,
-                                             typename Product<TapT, InT>::type (&acc)[R]) {
+                                             typename Product<TapT, InT>::type (&acc)[R],
+                                             const TapT* __restrict__ ltaps = nullptr) {
   using Geo = TileGeo<InT, D, R, WG>;
   constexpr int G = Geo::G;
   constexpr int CPR = D / G;  // granule columns per input row
@@ -351,13 +396,24 @@ __device__ __forceinline__ void poly_compute(const float4* __restrict__ lds, con
     const float4* __restrict__ seg = lds + (t + c * (JC / R)) * Geo::SGP;
 #pragma unroll
     for (int h = 0; h < CPR; ++h) {
-      // taps first (one SMEM batch, one wait), then the LDS window (in-order, counted waits)
-      const TapBuf tb = tap_window<TapT>(p.taps, p.T, c * JC * D + h * G);
       TapT tv[JC][G];
+      if constexpr (TAPS_LDS) {
+        // zero-padded taps staged in LDS: wave-uniform (broadcast) reads, in order with the window
+        // reads, so the compiler can count lgkmcnt instead of draining it
+        const TapT* tp = ltaps + c * JC * D + h * G;
 #pragma unroll
-      for (int j = 0; j < JC; ++j) {
+        for (int j = 0; j < JC; ++j) {
 #pragma unroll
-        for (int e = 0; e < G; ++e) tv[j][e] = tap_at<TapT>(tb, j * D + e);
+          for (int e = 0; e < G; ++e) tv[j][e] = tp[j * D + e];
+        }
+      } else {
+        // taps first (one SMEM batch, one wait), then the LDS window (in-order, counted waits)
+        const TapBuf tb = tap_window<TapT>(p.taps, p.T, c * JC * D + h * G);
+#pragma unroll
+        for (int j = 0; j < JC; ++j) {
+#pragma unroll
+          for (int e = 0; e < G; ++e) tv[j][e] = tap_at<TapT>(tb, j * D + e);
+        }
       }
       float4 win[NWIN];
 #pragma unroll
@@ -377,12 +433,25 @@ __device__ __forceinline__ void poly_compute(const float4* __restrict__ lds, con
   }
 }
 
+// Stage taps [0, span) into LDS, zero past T. Callers barrier before use.
+template <class TapT, int WG>
+__device__ __forceinline__ void stage_taps(TapT* __restrict__ ltaps, const FirParams& p, uint32_t span) {
+  const TapT* __restrict__ taps = reinterpret_cast<const TapT*>(p.taps);
+  for (uint32_t i = threadIdx.x; i < span; i += WG) {
+    TapT v;
+    set_zero(v);
+    if (i < p.T) v = taps[i];
+    ltaps[i] = v;
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // Kernel 1: polyphase-granule kernel, one tile per workgroup (D a multiple of the granule width G).
 // ABL (ablation, tuning probes only): 0 = full kernel, 1 = staging only, 2 = compute only.
 // NT: non-temporal (streaming) HBM loads for the staged input.
 // ------------------------------------------------------------------------------------------------
-template <class TapT, class InT, int D, int R, int JC, int WG, bool VEC, int MODE, int ABL = 0, bool NT = false>
+template <class TapT, class InT, int D, int R, int JC, int WG, bool VEC, int MODE, int ABL = 0, bool NT = false,
+          bool TL = false>
 __global__ __launch_bounds__(WG) void k_fir_poly(FirParams p) {
   using Geo = TileGeo<InT, D, R, WG>;
   using OutT = typename Product<TapT, InT>::type;
@@ -395,7 +464,9 @@ __global__ __launch_bounds__(WG) void k_fir_poly(FirParams p) {
   const uint64_t S0 = out0 * D;
   const uint32_t span = p.nch * JC * D;
   const uint32_t NG = ((Geo::KT - 1) * D + span + G - 1) / G;
-
+  // LDS: [tile granules | FM exchange (WG float2) | taps (span)]
+  TapT* ltaps = reinterpret_cast<TapT*>(lds + Geo::padded(NG - 1) + 1 + (WG * sizeof(float2) + 15) / 16);
+  if constexpr (TL) stage_taps<TapT, WG>(ltaps, p, span);
   if constexpr (ABL != 2) stage_tile<InT, Geo, WG, VEC, MODE, NT>(lds, in, S0, NG, p);
   __syncthreads();
 
@@ -407,11 +478,101 @@ __global__ __launch_bounds__(WG) void k_fir_poly(FirParams p) {
 #pragma unroll
     for (int r = 0; r < R; ++r) mac(acc[r], granule_sample<InT>(v, r % G), 1.0f);
   } else {
-    poly_compute<TapT, InT, D, R, JC, WG>(lds, p, acc);
+    poly_compute<TapT, InT, D, R, JC, WG, TL>(lds, p, acc, ltaps);
   }
 
   float2* xs = reinterpret_cast<float2*>(lds + Geo::padded(NG - 1) + 1);
-  tile_epilogue<MODE, OutT, R, WG>(p, out0, acc, xs);
+  tile_epilogue<MODE, OutT, R, WG, NT>(p, out0, acc, xs);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Kernel 1c: column-split polyphase kernel (D = 2G: two granule columns per row, e.g. complex D = 4).
+// Waves come in pairs over the same outputs: the even wave of a pair accumulates column 0 (phases
+// 0..G-1), the odd wave column 1. The column is wave-uniform, so a wave needs only NCH*JC*G taps --
+// 64 at T <= 128 -- which it loads into SGPRs once and keeps; the inner loop then issues nothing but
+// LDS window reads (in order, counted waits) and packed FMAs with SGPR tap operands. The odd wave
+// hands its partial sums to the even wave through a small LDS slab; the even wave stores.
+// ------------------------------------------------------------------------------------------------
+template <class TapT, class InT, int D, int R, int JC, int WG, int NCH, bool VEC, bool NT = false>
+__global__ __launch_bounds__(WG) void k_fir_poly_cs(FirParams p) {
+  constexpr int G = SampleT<InT>::kPerGranule;
+  static_assert(D == 2 * G, "two granule columns per row");
+  static_assert(WG % 128 == 0, "whole wave pairs");
+  constexpr int PAIRS = WG / 128;
+  using Geo = TileGeo<InT, D, R, PAIRS * 64>;  // one output segment per lane of a wave pair
+  using OutT = typename Product<TapT, InT>::type;
+  constexpr int NWIN = R + JC - 1;
+  static_assert(JC % R == 0, "chunk rows must be whole thread segments");
+
+  extern __shared__ __attribute__((aligned(16))) float4 lds[];
+  const InT* __restrict__ in = reinterpret_cast<const InT*>(p.in);
+  const uint64_t out0 = (uint64_t)blockIdx.x * p.tile_stride;
+  const uint64_t S0 = out0 * D;
+  const uint32_t span = NCH * JC * D;
+  const uint32_t NG = ((Geo::KT - 1) * D + span + G - 1) / G;
+  OutT* xs = reinterpret_cast<OutT*>(lds + Geo::padded(NG - 1) + 1);  // PAIRS*64*R partial sums
+
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t h = wave & 1u;          // this wave's granule column
+  const uint32_t pair = wave >> 1;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t seg = pair * 64u + lane;  // output segment within the tile
+
+  // this wave's taps, once: t[(c*JC + j)*D + h*G + e]
+  TapT tv[NCH][JC][G];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const TapBuf tb = tap_window<TapT>(p.taps, p.T, c * JC * D + h * G);
+#pragma unroll
+    for (int j = 0; j < JC; ++j) {
+#pragma unroll
+      for (int e = 0; e < G; ++e) tv[c][j][e] = tap_at<TapT>(tb, j * D + e);
+    }
+  }
+
+  stage_tile<InT, Geo, WG, VEC, kModeFir, NT>(lds, in, S0, NG, p);
+  __syncthreads();
+
+  OutT acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) set_zero(acc[r]);
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const float4* __restrict__ base = lds + (seg + c * (JC / R)) * Geo::SGP + h;
+    float4 win[NWIN];
+#pragma unroll
+    for (int u = 0; u < NWIN; ++u) {
+      const int q = u * 2;  // + h: even q and even SG keep the pad term independent of h
+      win[u] = base[q + Geo::PAD * (q / Geo::SG)];
+    }
+#pragma unroll
+    for (int j = 0; j < JC; ++j) {
+#pragma unroll
+      for (int e = 0; e < G; ++e) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) mac(acc[r], granule_sample<InT>(win[r + j], e), tv[c][j][e]);
+      }
+    }
+  }
+
+  if (h) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) xs[r * PAIRS * 64 + seg] = acc[r];
+  }
+  __syncthreads();
+  if (!h) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const OutT o = xs[r * PAIRS * 64 + seg];
+      if constexpr (sizeof(OutT) == 8) {
+        acc[r].x += o.x;
+        acc[r].y += o.y;
+      } else {
+        acc[r] += o;
+      }
+    }
+    store_fir<OutT, R, NT>(reinterpret_cast<OutT*>(p.out), out0 + seg * R, p.N, acc);
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -517,6 +678,106 @@ __global__ __launch_bounds__(WG, 4) void k_fir_poly_pipe(FirParams p, uint32_t n
 }
 
 // ------------------------------------------------------------------------------------------------
+// Kernel 1d: persistent, double-buffered LDS-DMA pipeline (FIR mode). HBM -> LDS with
+// buffer_load_dwordx4 ... lds (no VGPR round trip, no ds_write): while a workgroup computes tile i
+// out of one LDS buffer, its waves' DMA for tile i+1 fills the other. The DMA is issued from inline
+// asm so the compiler does not serialise every ds_read behind it (its waitcnt pass cannot tell the
+// two buffers apart); completion is awaited by hand: s_waitcnt vmcnt(0), then the barrier.
+// Pad slots of the padded layout and granules past the input's end are fetched from an
+// out-of-range offset, which the buffer range check turns into zeros.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t lds_byte_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+__device__ __forceinline__ void dma16_nt(uint32_t lds_base, uint32_t voff, gsdr_v4i32 rsrc) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, 0 offen nt lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(rsrc), "s"(lds_base)
+      : "memory");
+}
+
+template <int SG, int SGP>
+__device__ __forceinline__ uint32_t slot_source_offset(uint32_t s, uint32_t NGP) {
+  const uint32_t seg = s / SGP;
+  const uint32_t w = s - seg * SGP;
+  return (w < (uint32_t)SG && s < NGP) ? (seg * SG + w) * 16u : 0x80000000u;
+}
+
+template <class InT, class Geo, int WG>
+__device__ __forceinline__ void dma_tile(float4* buf, uint32_t slots, const InT* __restrict__ in, uint64_t S0,
+                                         uint32_t NG, uint32_t NGP, const FirParams& p) {
+  constexpr int G = Geo::G;
+  const uint64_t avail = p.L > S0 ? p.L - S0 : 0;
+  const uint32_t nrec = avail >= (uint64_t)NG * G ? NG * 16u : (uint32_t)(avail / G) * 16u;
+  const uint64_t a = reinterpret_cast<uint64_t>(in + S0);
+  const gsdr_v4i32 rsrc = gsdr_v4i32{(int)(uint32_t)a, (int)(uint32_t)(a >> 32) & 0xffff, (int)nrec, 0x00020000};
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t base = lds_byte_addr(buf) + wave * 64u * 16u;
+  for (uint32_t k = 0; k < slots; k += WG) {
+    const uint32_t s = k + wave * 64u + lane;
+    dma16_nt(base + k * 16u, slot_source_offset<Geo::SG, Geo::SGP>(s, NGP), rsrc);
+  }
+}
+
+// The one granule that straddles the input's end (odd sample count) is not whole, so the range
+// check zeroed it; rewrite it from memory (last tile only). Caller barriers after.
+template <class InT, class Geo, int WG>
+__device__ __forceinline__ bool dma_fixup(float4* buf, const InT* __restrict__ in, uint64_t S0, uint32_t NG,
+                                          const FirParams& p) {
+  constexpr int G = Geo::G;
+  const uint64_t avail = p.L > S0 ? p.L - S0 : 0;
+  if (!(avail < (uint64_t)NG * G && avail % G != 0)) return false;
+  const uint32_t gl = (uint32_t)(avail / G);
+  if (gl % WG == threadIdx.x) buf[Geo::padded(gl)] = load_granule<InT, false>(in, S0 + (uint64_t)gl * G, p.L);
+  return true;
+}
+
+template <class TapT, class InT, int D, int R, int JC, int WG, bool TL = false>
+__global__ __launch_bounds__(WG) void k_fir_poly_dma(FirParams p, uint32_t ntiles, uint32_t slots) {
+  using Geo = TileGeo<InT, D, R, WG>;
+  using OutT = typename Product<TapT, InT>::type;
+  constexpr int G = Geo::G;
+  extern __shared__ __attribute__((aligned(16))) float4 lds[];
+  const InT* __restrict__ in = reinterpret_cast<const InT*>(p.in);
+  const uint32_t span = p.nch * JC * D;
+  const uint32_t NG = ((Geo::KT - 1) * D + span + G - 1) / G;
+  const uint32_t NGP = Geo::padded(NG - 1) + 1;
+  TapT* ltaps = reinterpret_cast<TapT*>(lds + 2 * slots);
+
+  uint32_t tile = blockIdx.x;
+  if (tile >= ntiles) return;
+  if constexpr (TL) stage_taps<TapT, WG>(ltaps, p, span);
+  dma_tile<InT, Geo, WG>(lds, slots, in, (uint64_t)tile * p.tile_stride * D, NG, NGP, p);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (dma_fixup<InT, Geo, WG>(lds, in, (uint64_t)tile * p.tile_stride * D, NG, p)) __syncthreads();
+  for (uint32_t it = 0;; ++it) {
+    float4* cur = lds + (it & 1u) * slots;
+    float4* nxt = lds + ((it + 1u) & 1u) * slots;
+    const uint32_t next = tile + gridDim.x;
+    if (next < ntiles) dma_tile<InT, Geo, WG>(nxt, slots, in, (uint64_t)next * p.tile_stride * D, NG, NGP, p);
+    OutT acc[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) set_zero(acc[r]);
+    poly_compute<TapT, InT, D, R, JC, WG, TL>(cur, p, acc, ltaps);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of the next tile has landed
+    tile_epilogue<kModeFir, OutT, R, WG>(p, (uint64_t)tile * p.tile_stride, acc, nullptr);
+    __syncthreads();  // every wave's DMA landed, and nobody still reads `cur`
+    if (next >= ntiles) break;
+    if (dma_fixup<InT, Geo, WG>(nxt, in, (uint64_t)next * p.tile_stride * D, NG, p)) __syncthreads();
+    tile = next;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Kernel 2: contiguous-window kernel for small D (D = 1 in particular).
 //   IC = taps per chunk (a multiple of R*D).
 // ------------------------------------------------------------------------------------------------
@@ -585,7 +846,7 @@ __device__ __forceinline__ typename Product<TapT, InT>::type fir_point(const Fir
   for (uint32_t i = 0; i < p.T; ++i) {
     InT x = in[s0 + i];
     if constexpr (MODE != kModeFir) {
-      x = nco_mix(x, (p.nco_n0 + (uint32_t)(s0 + i)) * p.nco_inc);
+      x = nco_mix(x, p.nco_n0 + (uint32_t)(s0 + i), p.nco_inc);
     }
     mac(acc, x, taps[i]);
   }
@@ -612,12 +873,12 @@ __global__ __launch_bounds__(256) void k_fir_generic(FirParams p) {
 // Host-side sizing helpers
 // ------------------------------------------------------------------------------------------------
 template <class InT, int D, int R, int WG>
-inline size_t poly_lds_bytes(uint32_t span_samples, int mode) {
+inline size_t poly_lds_bytes(uint32_t span_samples, int mode, size_t tap_bytes = 0) {
   using Geo = TileGeo<InT, D, R, WG>;
   const uint32_t NG = ((Geo::KT - 1) * D + span_samples + Geo::G - 1) / Geo::G;
   size_t bytes = (size_t)(Geo::padded(NG - 1) + 1) * 16u;
-  if (mode == kModeFm) bytes += (size_t)WG * sizeof(float2);
-  return bytes;
+  if (mode != kModeFir || tap_bytes) bytes += ((size_t)WG * sizeof(float2) + 15) / 16 * 16;
+  return bytes + tap_bytes;
 }
 
 }  // namespace gsdr

@@ -10,7 +10,7 @@ from __future__ import annotations
 import ctypes
 import os
 
-__all__ = ["lib", "LIB_PATH", "SIGNATURES", "GsdrError", "check"]
+__all__ = ["lib", "LIB_PATH", "SIGNATURES", "GsdrError", "Complex", "check"]
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgsdr.so")
 
@@ -21,6 +21,15 @@ _i32 = ctypes.c_int32
 _int = ctypes.c_int
 _f = ctypes.c_float
 _err = ctypes.c_int  # hipError_t
+
+
+class Complex(ctypes.Structure):
+    """hipFloatComplex passed by value (two floats, 8-byte aligned)."""
+
+    _fields_ = [("x", ctypes.c_float), ("y", ctypes.c_float)]
+
+
+_c = Complex
 
 # name -> (restype, argtypes), in the order of include/gsdr/*.h
 SIGNATURES = {
@@ -36,6 +45,19 @@ SIGNATURES = {
     "gsdrQuadFmDemod": (_err, [_p, _p, _f, _sz, _i32, _p]),
     "gsdrQuadAmDemod": (_err, [_p, _p, _sz, _i32, _p]),
     "gsdrMagnitude": (_err, [_p, _p, _sz, _i32, _p]),
+    "gsdrAddConstFF": (_err, [_p, _f, _p, _sz, _i32, _p]),
+    "gsdrAddConstCC": (_err, [_p, _c, _p, _sz, _i32, _p]),
+    "gsdrAddConstCF": (_err, [_p, _f, _p, _sz, _i32, _p]),
+    "gsdrAddConstFC": (_err, [_p, _c, _p, _sz, _i32, _p]),
+    "gsdrMultiplyCC": (_err, [_p, _p, _p, _sz, _i32, _p]),
+    "gsdrMultiplyFF": (_err, [_p, _p, _p, _sz, _i32, _p]),
+    "gsdrMultiplyCF": (_err, [_p, _p, _p, _sz, _i32, _p]),
+    "gsdrAddToMagnitude": (_err, [_p, _f, _p, _sz, _i32, _p]),
+    "gsdrAbs": (_err, [_p, _p, _sz, _i32, _p]),
+    # trig.h / conversion.h
+    "gsdrCosineC": (_err, [_f, _f, _p, _sz, _i32, _p]),
+    "gsdrCosineF": (_err, [_f, _f, _p, _sz, _i32, _p]),
+    "gsdrInt8ToNormFloat": (_err, [_p, _p, _sz, _i32, _p]),
     # qpsk.h
     "gsdrQpskModulate": (_err, [_p, _p, _u32, _f, _i32, _p]),
     "gsdrQpskModulate4x": (_err, [_p, _p, _p, _p, _p, _p, _p, _p, _u32, _f, _i32, _p]),

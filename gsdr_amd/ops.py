@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import torch
 
-from .abi import check, lib
+from .abi import Complex, check, lib
 
 __all__ = [
     "fir", "fir_variant", "fm_demod", "am_demod", "quad_fm_demod", "quad_am_demod", "magnitude",
@@ -17,6 +17,7 @@ __all__ = [
     "qpsk_modulate_templated", "qpsk_demodulate_templated",
     "qpsk256_init", "qpsk256_modulate", "qpsk256_demodulate", "qpsk256_modulate_4x", "qpsk256_demodulate_4x",
     "nco_phase_increment", "stream_of",
+    "add_const", "multiply", "add_to_magnitude", "abs_", "cosine", "int8_to_norm_float",
 ]
 
 
@@ -152,6 +153,88 @@ def magnitude(x, out=None):
     out = torch.empty(n, dtype=torch.float32, device=x.device) if out is None else out
     _require(out, torch.float32, "output", n)
     check("gsdrMagnitude", lib.gsdrMagnitude(_ptr(x), _ptr(out), n, _dev(x), stream_of(x)))
+    return out
+
+
+_ADD = {
+    (torch.float32, False): ("gsdrAddConstFF", torch.float32),
+    (torch.complex64, True): ("gsdrAddConstCC", torch.complex64),
+    (torch.complex64, False): ("gsdrAddConstCF", torch.complex64),
+    (torch.float32, True): ("gsdrAddConstFC", torch.complex64),
+}
+
+
+def add_const(x, c, out=None):
+    """gsdrAddConst{FF,CC,CF,FC}: the variant follows x's dtype and whether c is complex."""
+    is_c = isinstance(c, complex)
+    if (x.dtype, is_c) not in _ADD:
+        raise TypeError(f"unsupported input dtype {x.dtype}")
+    name, odt = _ADD[(x.dtype, is_c)]
+    _require(x, x.dtype, "input")
+    n = x.numel()
+    out = torch.empty(n, dtype=odt, device=x.device) if out is None else out
+    _require(out, odt, "output", n)
+    cval = Complex(c.real, c.imag) if is_c else float(c)
+    check(name, getattr(lib, name)(_ptr(x), cval, _ptr(out), n, _dev(x), stream_of(x)))
+    return out
+
+
+_MUL = {
+    (torch.complex64, torch.complex64): ("gsdrMultiplyCC", torch.complex64),
+    (torch.float32, torch.float32): ("gsdrMultiplyFF", torch.float32),
+    (torch.complex64, torch.float32): ("gsdrMultiplyCF", torch.complex64),
+}
+
+
+def multiply(a, b, out=None):
+    key = (a.dtype, b.dtype)
+    if key not in _MUL:
+        raise TypeError(f"unsupported dtypes {key}")
+    name, odt = _MUL[key]
+    n = a.numel()
+    _require(a, a.dtype, "in1")
+    _require(b, b.dtype, "in2", n)
+    out = torch.empty(n, dtype=odt, device=a.device) if out is None else out
+    _require(out, odt, "out", n)
+    check(name, getattr(lib, name)(_ptr(a), _ptr(b), _ptr(out), n, _dev(a), stream_of(a)))
+    return out
+
+
+def add_to_magnitude(x, c, out=None):
+    _require(x, torch.complex64, "input")
+    n = x.numel()
+    out = torch.empty(n, dtype=torch.complex64, device=x.device) if out is None else out
+    _require(out, torch.complex64, "output", n)
+    check("gsdrAddToMagnitude", lib.gsdrAddToMagnitude(_ptr(x), float(c), _ptr(out), n, _dev(x), stream_of(x)))
+    return out
+
+
+def abs_(x, out=None):
+    _require(x, torch.float32, "in")
+    n = x.numel()
+    out = torch.empty(n, dtype=torch.float32, device=x.device) if out is None else out
+    _require(out, torch.float32, "out", n)
+    check("gsdrAbs", lib.gsdrAbs(_ptr(x), _ptr(out), n, _dev(x), stream_of(x)))
+    return out
+
+
+def cosine(phi_begin, phi_end, n, complex_out=True, device=None, out=None):
+    """gsdrCosineC / gsdrCosineF: a phase ramp from phi_begin towards phi_end over n samples."""
+    odt = torch.complex64 if complex_out else torch.float32
+    device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    out = torch.empty(n, dtype=odt, device=device) if out is None else out
+    _require(out, odt, "output", n)
+    name = "gsdrCosineC" if complex_out else "gsdrCosineF"
+    check(name, getattr(lib, name)(float(phi_begin), float(phi_end), _ptr(out), n, _dev(out), stream_of(out)))
+    return out
+
+
+def int8_to_norm_float(x, out=None):
+    _require(x, torch.int8, "input")
+    n = x.numel()
+    out = torch.empty(n, dtype=torch.float32, device=x.device) if out is None else out
+    _require(out, torch.float32, "output", n)
+    check("gsdrInt8ToNormFloat", lib.gsdrInt8ToNormFloat(_ptr(x), _ptr(out), n, _dev(x), stream_of(x)))
     return out
 
 

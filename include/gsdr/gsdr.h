@@ -6,6 +6,7 @@
 
 #include <gsdr/am.h>
 #include <gsdr/arithmetic.h>
+#include <gsdr/conversion.h>
 #include <gsdr/fir.h>
 #include <gsdr/fm.h>
 #include <gsdr/gsdr_ext.h>
@@ -13,6 +14,7 @@
 #include <gsdr/qpsk.h>
 #include <gsdr/qpsk256.h>
 #include <gsdr/quad_demod.h>
+#include <gsdr/trig.h>
 #include <gsdr/util.h>
 
 #endif /* GSDR_GSDR_H_ */

@@ -305,3 +305,69 @@ void oracle_qpsk256_demod_hypot(const float* table, const float* in, uint8_t* ou
     out[k] = (uint8_t)idx;
   }
 }
+
+/* ---------------------------------------------------------------- element-wise maps */
+
+/* reference src/add_const.cu:20-28 (k_AddConst: out = addConst + input) */
+void oracle_add_const(int variant, const float* x, float cr, float ci, float* out, size_t n) {
+  for (size_t k = 0; k < n; ++k) {
+    switch (variant) {
+      case 0: out[k] = cr + x[k]; break;
+      case 1: out[2 * k] = cr + x[2 * k]; out[2 * k + 1] = ci + x[2 * k + 1]; break;
+      case 2: out[2 * k] = x[2 * k] + cr; out[2 * k + 1] = x[2 * k + 1]; break; /* operator+(c, r) */
+      default: out[2 * k] = cr + x[k]; out[2 * k + 1] = ci; break;              /* operator+(c, r) */
+    }
+  }
+}
+
+/* reference src/multiply.cu:20-27 (in1 * in2; cuCmulf for complex x complex) */
+void oracle_multiply(int variant, const float* a, const float* b, float* out, size_t n) {
+  for (size_t k = 0; k < n; ++k) {
+    if (variant == 0) {
+      const float ar = a[2 * k], ai = a[2 * k + 1], br = b[2 * k], bi = b[2 * k + 1];
+      out[2 * k] = ar * br - ai * bi;
+      out[2 * k + 1] = ar * bi + ai * br;
+    } else if (variant == 1) {
+      out[k] = a[k] * b[k];
+    } else {
+      out[2 * k] = a[2 * k] * b[k];
+      out[2 * k + 1] = a[2 * k + 1] * b[k];
+    }
+  }
+}
+
+/* reference src/add_const.cu:30-42 */
+void oracle_add_to_magnitude(const float* x, float c, float* out, size_t n) {
+  for (size_t k = 0; k < n; ++k) {
+    const float m = hypotf(x[2 * k], x[2 * k + 1]);
+    const float nx = x[2 * k] / m, ny = x[2 * k + 1] / m;
+    const float len = c + m;
+    out[2 * k] = nx * len;
+    out[2 * k + 1] = ny * len;
+  }
+}
+
+/* reference src/magnitude.cu:30-36 */
+void oracle_abs(const float* x, float* out, size_t n) {
+  for (size_t k = 0; k < n; ++k) out[k] = fabsf(x[k]);
+}
+
+/* reference src/conversion.cu:20-27 */
+void oracle_int8_to_float(const int8_t* x, float* out, size_t n) {
+  for (size_t k = 0; k < n; ++k) out[k] = fmaxf(-1.0f, (float)x[k] / 127.0f);
+}
+
+/* reference src/trig.cu:20-45 (kernels) and :55, :70 (host step); theta as nvcc contracts it */
+void oracle_cosine(int complex_out, float phi_begin, float phi_end, float* out, size_t n) {
+  if (n == 0) return;
+  const float m = (float)((phi_end - phi_begin) / (double)n);
+  for (size_t k = 0; k < n; ++k) {
+    const float th = fmaf((float)(uint32_t)k, m, phi_begin);
+    if (complex_out) {
+      out[2 * k] = cosf(th);
+      out[2 * k + 1] = sinf(th);
+    } else {
+      out[k] = cosf(th);
+    }
+  }
+}

@@ -75,4 +75,17 @@ void oracle_qpsk256_demod_hypot(const float* table, const float* in, uint8_t* ou
 }
 #endif
 
+
+/* Element-wise maps: reference src/add_const.cu:20-42, multiply.cu:20-27,
+ * magnitude.cu:30-36, trig.cu:20-75, conversion.cu:20-35, with the operator semantics of
+ * src/cuComplexOperatorOverloads.cuh:25-56. Complex arrays are interleaved float pairs.
+ * add_const variant: 0 FF, 1 CC, 2 CF (complex + real: real part only), 3 FC (real + complex).
+ * multiply variant: 0 CC (cuCmulf), 1 FF, 2 CF. */
+void oracle_add_const(int variant, const float* x, float cr, float ci, float* out, size_t n);
+void oracle_multiply(int variant, const float* a, const float* b, float* out, size_t n);
+void oracle_add_to_magnitude(const float* x, float c, float* out, size_t n);
+void oracle_abs(const float* x, float* out, size_t n);
+void oracle_int8_to_float(const int8_t* x, float* out, size_t n);
+void oracle_cosine(int complex_out, float phi_begin, float phi_end, float* out, size_t n);
+
 #endif /* GSDR_ORACLE_H_ */

@@ -38,6 +38,12 @@ _SIG = {
     "oracle_qpsk256_mod": [_p, _p, _p, _u32],
     "oracle_qpsk256_demod": [_p, _p, _p, _u32],
     "oracle_qpsk256_demod_hypot": [_p, _p, _p, _u32],
+    "oracle_add_const": [_int, _p, _f, _f, _p, _sz],
+    "oracle_multiply": [_int, _p, _p, _p, _sz],
+    "oracle_add_to_magnitude": [_p, _f, _p, _sz],
+    "oracle_abs": [_p, _p, _sz],
+    "oracle_int8_to_float": [_p, _p, _sz],
+    "oracle_cosine": [_int, _f, _f, _p, _sz],
 }
 for _name, _args in _SIG.items():
     getattr(_lib, _name).argtypes = _args
@@ -198,4 +204,53 @@ def qpsk256_demod(table, x, rule="sq"):
     out = np.empty(x.size, dtype=np.uint8)
     fn = _lib.oracle_qpsk256_demod if rule == "sq" else _lib.oracle_qpsk256_demod_hypot
     fn(_ptr(table), _ptr(x), _ptr(out), x.size)
+    return out
+
+
+def add_const(x, c):
+    """gsdrAddConst{FF,CC,CF,FC} by x's dtype and whether c is complex."""
+    is_c = isinstance(c, complex)
+    cplx_in = np.iscomplexobj(x)
+    x = _c(x, np.complex64 if cplx_in else np.float32)
+    variant = {(False, False): 0, (True, True): 1, (True, False): 2, (False, True): 3}[(cplx_in, is_c)]
+    out = np.empty(x.size, np.complex64 if (cplx_in or is_c) else np.float32)
+    cr, ci = (c.real, c.imag) if is_c else (float(c), 0.0)
+    _lib.oracle_add_const(variant, _ptr(x), cr, ci, _ptr(out), x.size)
+    return out
+
+
+def multiply(a, b):
+    ca, cb = np.iscomplexobj(a), np.iscomplexobj(b)
+    variant = {(True, True): 0, (False, False): 1, (True, False): 2}[(ca, cb)]
+    a = _c(a, np.complex64 if ca else np.float32)
+    b = _c(b, np.complex64 if cb else np.float32)
+    out = np.empty(a.size, np.complex64 if ca else np.float32)
+    _lib.oracle_multiply(variant, _ptr(a), _ptr(b), _ptr(out), a.size)
+    return out
+
+
+def add_to_magnitude(x, c):
+    x = _c(x, np.complex64)
+    out = np.empty(x.size, np.complex64)
+    _lib.oracle_add_to_magnitude(_ptr(x), float(c), _ptr(out), x.size)
+    return out
+
+
+def abs_(x):
+    x = _c(x, np.float32)
+    out = np.empty(x.size, np.float32)
+    _lib.oracle_abs(_ptr(x), _ptr(out), x.size)
+    return out
+
+
+def int8_to_float(x):
+    x = _c(x, np.int8)
+    out = np.empty(x.size, np.float32)
+    _lib.oracle_int8_to_float(_ptr(x), _ptr(out), x.size)
+    return out
+
+
+def cosine(phi_begin, phi_end, n, complex_out=True):
+    out = np.empty(n, np.complex64 if complex_out else np.float32)
+    _lib.oracle_cosine(1 if complex_out else 0, float(phi_begin), float(phi_end), _ptr(out), n)
     return out

@@ -141,6 +141,44 @@ def main():
         best[allinf] = 0  # strict '<' against +inf never fires
         save(f"qpsk256_{name}", table=tab, symbols=syms, tx=tx, rx=rx, demod=best)
 
+    elementwise()
+
+
+def elementwise():
+    """reference src/add_const.cu:20-42, multiply.cu:20-27, magnitude.cu:30-36, conversion.cu:20-27,
+    trig.cu:20-75 with the operator semantics of src/cuComplexOperatorOverloads.cuh:25-56. numpy float32
+    arithmetic rounds each operation (no contraction), which is the build's contract for the exact maps;
+    hypot and cos/sin come from float64 and are compared within a tolerance."""
+    rng = np.random.default_rng(0xE1E)
+    n = 1000
+    f32 = np.float32
+    x = rng.uniform(-10, 10, n).astype(f32)
+    x[:6] = [0.0, -0.0, 1.0, -1.0, np.inf, -np.inf]
+    y = rng.uniform(-10, 10, n).astype(f32)
+    xc = (rng.uniform(-10, 10, n) + 1j * rng.uniform(-10, 10, n)).astype(np.complex64)
+    yc = (rng.uniform(-10, 10, n) + 1j * rng.uniform(-10, 10, n)).astype(np.complex64)
+    cf, cc = f32(3.14), np.complex64(1.5 - 2.5j)
+    xr, xi, yr, yi = xc.real, xc.imag, yc.real, yc.imag
+    add_ff = (cf + x).astype(f32)
+    add_cc = ((cc.real + xr) + 1j * (cc.imag + xi)).astype(np.complex64)
+    add_cf = ((xr + cf) + 1j * xi).astype(np.complex64)            # real part only
+    add_fc = ((cc.real + x) + 1j * np.full(n, cc.imag, f32)).astype(np.complex64)
+    mul_cc = ((xr * yr - xi * yi) + 1j * (xr * yi + xi * yr)).astype(np.complex64)
+    mul_ff = (x * y).astype(f32)
+    mul_cf = ((xr * y) + 1j * (xi * y)).astype(np.complex64)
+    m64 = np.hypot(xr.astype(np.float64), xi.astype(np.float64))
+    a2m = (xc.astype(np.complex128) / m64 * (2.5 + m64)).astype(np.complex64)
+    i8 = np.arange(-128, 128, dtype=np.int8)
+    conv = np.maximum(f32(-1.0), i8.astype(f32) / f32(127.0)).astype(f32)
+    phi0, phi1, nc = f32(-1.3), f32(40.0), 1000
+    step = f32((phi1 - phi0) / np.float64(nc))  # float subtraction, double division (trig.cu:55)
+    th = (np.arange(nc, dtype=np.float64) * np.float64(step) + np.float64(phi0)).astype(f32)
+    cos_c = (np.cos(th.astype(np.float64)) + 1j * np.sin(th.astype(np.float64))).astype(np.complex64)
+    save("elementwise", x=x, y=y, xc=xc, yc=yc, cf=np.array([cf]), cc=np.array([cc]), add_ff=add_ff,
+         add_cc=add_cc, add_cf=add_cf, add_fc=add_fc, mul_cc=mul_cc, mul_ff=mul_ff, mul_cf=mul_cf,
+         a2m_c=np.array([f32(2.5)]), a2m=a2m, abs=np.abs(x).astype(f32), i8=i8, conv=conv,
+         phi=np.array([phi0, phi1]), cos_c=cos_c)
+
 
 if __name__ == "__main__":
     main()

@@ -41,7 +41,10 @@ def test_headers_declare_the_reference_surface():
            "gsdrQuadAmDemod", "gsdrMagnitude", "gsdrQpskModulate", "gsdrQpskModulate4x", "gsdrQpskDemodulate",
            "gsdrQpskDemodulate4x", "gsdrQpskModulateTemplated", "gsdrQpskDemodulateTemplated",
            "gsdrQpsk256Modulate", "gsdrQpsk256Demodulate", "gsdrQpsk256Modulate4x", "gsdrQpsk256Demodulate4x",
-           "gsdrQpsk256InitConstellation"]
+           "gsdrQpsk256InitConstellation",
+           # element-wise surface: arithmetic.h:26-95, trig.h, conversion.h
+           "gsdrAddConstFF", "gsdrAddConstCC", "gsdrAddConstCF", "gsdrAddConstFC", "gsdrMultiplyCC", "gsdrMultiplyFF",
+           "gsdrMultiplyCF", "gsdrAddToMagnitude", "gsdrAbs", "gsdrCosineC", "gsdrCosineF", "gsdrInt8ToNormFloat"]
     for n in ref:
         assert n in names, n
     # argument counts of the reference headers (fir.h:30-68, fm.h:42-55, am.h:25-37, ...)

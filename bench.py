@@ -148,9 +148,32 @@ def settle_clocks(torch, step, max_launches, window=25, tol=0.02):
     return n
 
 
+def time_abi(torch, fn, argsets, reps=50, settle=400):
+    """Per-launch time of a C-ABI call rotating over pre-marshalled argument sets (one per input
+    batch): untimed warm-up + clock settle, then `reps` launches inside one HIP event pair."""
+    cnt = [0]
+
+    def step():
+        rc = fn(*argsets[cnt[0] % len(argsets)])
+        cnt[0] += 1
+        assert rc == 0, rc
+
+    for _ in range(5):
+        step()
+    settle_clocks(torch, step, settle)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        step()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps * 1e-3
+
+
 def secondary_configs(torch, ops, device, taps):
-    """Config 3 (fused NCO + FIR + FM, 64 M samples) and config 5 (QPSK256 16 M symbols): kernel
-    times from HIP events, reported beside the headline line."""
+    """Config 3 (fused NCO + FIR + FM, 64 M samples), the int8 I/Q front end on
+    the config-2 and config-3 shapes, and config 5 (QPSK256 16 M symbols): kernel times from HIP
+    events, reported beside the headline line."""
     import numpy as np
 
     from gsdr_amd import abi
@@ -160,34 +183,37 @@ def secondary_configs(torch, ops, device, taps):
     n_fm = (1 << 24) - 1
     n_in = n_fm * DECIM + TAPS
     g = torch.Generator(device=device).manual_seed(0x5EED)
+    stream = torch.cuda.current_stream(device).cuda_stream
     xs = [(torch.rand(2 * n_in, device=device, generator=g) * 2 - 1).view(torch.complex64) for _ in range(ROTATE)]
     y = torch.empty(n_fm, dtype=torch.float32, device=device)
-    stream = torch.cuda.current_stream(device).cuda_stream
     argsets = [(fs, tune, chan, dev_hz, DECIM, 0, taps.data_ptr(), TAPS, x.data_ptr(), y.data_ptr(), n_fm,
                 device.index, stream) for x in xs]
-    cnt = [0]
-
-    def fm_step():
-        rc = abi.lib.gsdrFmDemod(*argsets[cnt[0] % ROTATE])
-        cnt[0] += 1
-        assert rc == 0, rc
-
-    for _ in range(5):
-        fm_step()
-    settle_clocks(torch, fm_step, 400)
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    reps = 50
-    s.record()
-    for _ in range(reps):
-        fm_step()
-    e.record()
-    torch.cuda.synchronize()
-    t = s.elapsed_time(e) / reps * 1e-3
+    t = time_abi(torch, abi.lib.gsdrFmDemod, argsets)
     b = 8 * n_in + 4 * n_fm + 4 * TAPS
     out["fm_chain"] = {"config": "NCO + 127-tap FIR (D=4) + FM discriminator, 67,108,987 samples (BASELINE configs[2])",
                        "us_per_launch": round(t * 1e6, 2), "msamples_per_s": round(n_in / t / 1e6, 1),
                        "alg_gbps": round(b / t / 1e9, 1), "alg_bytes_per_launch": b}
     del xs
+    # int8 I/Q front end fused into the filter: 2 instead of 8 input bytes per sample
+    x8s = [torch.randint(-128, 128, (2 * n_in,), dtype=torch.int8, device=device, generator=g) for _ in range(ROTATE)]
+    argsets = [(fs, tune, chan, dev_hz, DECIM, 0, taps.data_ptr(), TAPS, x.data_ptr(), y.data_ptr(), n_fm,
+                device.index, stream) for x in x8s]
+    t = time_abi(torch, abi.lib.gsdrxFmDemodInt8, argsets)
+    b = 2 * n_in + 4 * n_fm + 4 * TAPS
+    out["fm_chain_int8"] = {"config": "config 3 from int8 I/Q (gsdrxFmDemodInt8)", "us_per_launch": round(t * 1e6, 2),
+                            "msamples_per_s": round(n_in / t / 1e6, 1), "alg_gbps": round(b / t / 1e9, 1),
+                            "alg_bytes_per_launch": b}
+    del y
+    yf = torch.empty(N_OUT, dtype=torch.complex64, device=device)
+    argsets = [(DECIM, taps.data_ptr(), TAPS, x.data_ptr(), yf.data_ptr(), N_OUT, device.index, stream) for x in x8s]
+    t = time_abi(torch, abi.lib.gsdrxFirFCInt8, argsets)
+    b = 2 * N_IN + 8 * N_OUT + 4 * TAPS
+    out["fir_int8"] = {"config": "config 2 from int8 I/Q (gsdrxFirFCInt8), 67,108,987 samples",
+                       "us_per_launch": round(t * 1e6, 2), "msamples_per_s": round(N_IN / t / 1e6, 1),
+                       "alg_gbps": round(b / t / 1e9, 1), "alg_bytes_per_launch": b,
+                       "fma_tflops": round(4 * TAPS * N_OUT / t / 1e12, 1)}
+    del x8s, yf
+    reps = 50
     n = 1 << 24
     ops.qpsk256_init(0, 1.0, device.index)
     syms = torch.randint(0, 256, (n,), dtype=torch.uint8, device=device, generator=g)

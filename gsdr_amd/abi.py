@@ -75,6 +75,16 @@ SIGNATURES = {
     "gsdrVersion": (ctypes.c_char_p, []),
     "gsdrNcoPhaseIncrement": (_u32, [_f, _f, _f]),
     "gsdrxFirFCVariant": (_err, [_int, _sz, _p, _sz, _p, _p, _sz, _i32, _p]),
+    "gsdrxFirFCInt8": (_err, [_sz, _p, _sz, _p, _p, _sz, _i32, _p]),
+    "gsdrxFirFCInt8Variant": (_err, [_int, _sz, _p, _sz, _p, _p, _sz, _i32, _p]),
+    "gsdrxFmDemodInt8": (_err, [_f, _f, _f, _f, _u32, _sz, _p, _sz, _p, _p, _sz, _i32, _p]),
+    # stream.h
+    "gsdrxStreamCreate": (_err, [ctypes.POINTER(_p), _int, _int, _u32, _p, _sz, _f, _f, _f, _f, _sz, _i32]),
+    "gsdrxStreamOutputsFor": (_sz, [_p, _sz]),
+    "gsdrxStreamProcess": (_err, [_p, _p, _sz, _p, _sz, ctypes.POINTER(_sz), _p]),
+    "gsdrxStreamDestroy": (_err, [_p]),
+    "gsdrxStreamPlan": (None, [_u32, _sz, ctypes.c_uint64, ctypes.c_uint64, _sz, ctypes.POINTER(ctypes.c_uint64)]),
+    "gsdrxAmDemodInt8": (_err, [_f, _f, _f, _u32, _sz, _p, _sz, _p, _p, _sz, _i32, _p]),
 }
 
 

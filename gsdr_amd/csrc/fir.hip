@@ -111,6 +111,20 @@ GSDR_C_LINKAGE hipError_t gsdrFirFC(size_t decimation, const float* taps, size_t
   return fir_entry<float, float2>(decimation, taps, tapCount, input, output, numOutputs, cudaDevice, cudaStream, -1);
 }
 
+GSDR_C_LINKAGE hipError_t gsdrxFirFCInt8(size_t decimation, const float* taps, size_t tapCount, const int8_t* input,
+                                         hipFloatComplex* output, size_t numOutputs, int32_t cudaDevice,
+                                         hipStream_t cudaStream) GSDR_NO_EXCEPT {
+  return fir_entry<float, gsdr::Iq8>(decimation, taps, tapCount, reinterpret_cast<const gsdr::Iq8*>(input), output,
+                                     numOutputs, cudaDevice, cudaStream, -1);
+}
+
+GSDR_C_LINKAGE hipError_t gsdrxFirFCInt8Variant(int variant, size_t decimation, const float* taps, size_t tapCount,
+                                                const int8_t* input, hipFloatComplex* output, size_t numOutputs,
+                                                int32_t cudaDevice, hipStream_t cudaStream) GSDR_NO_EXCEPT {
+  return fir_entry<float, gsdr::Iq8>(decimation, taps, tapCount, reinterpret_cast<const gsdr::Iq8*>(input), output,
+                                     numOutputs, cudaDevice, cudaStream, variant < 0 ? -1 : variant);
+}
+
 GSDR_C_LINKAGE hipError_t gsdrFirFF(size_t decimation, const float* taps, size_t tapCount, const float* input,
                                     float* output, size_t numOutputs, int32_t cudaDevice,
                                     hipStream_t cudaStream) GSDR_NO_EXCEPT {

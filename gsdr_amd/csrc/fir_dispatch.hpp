@@ -77,7 +77,8 @@ hipError_t launch_poly(const FirJob& j, hipStream_t s) {
   p.tile_stride = stride;
   const uint64_t tiles = ceil_div<uint64_t>(j.N, stride);
   if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
-  const bool vec = aligned16(j.in) && ((uint64_t)stride * D * sizeof(InT)) % 16 == 0;
+  constexpr uint64_t A = SampleT<InT>::kSrcAlign;
+  const bool vec = (reinterpret_cast<uintptr_t>(j.in) % A) == 0 && ((uint64_t)stride * D * sizeof(InT)) % A == 0;
   if (vec) {
     k_fir_poly<TapT, InT, D, R, JC, WG, true, MODE, ABL, NT, TL><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
   } else {
@@ -309,12 +310,58 @@ hipError_t launch_d4_complex(const FirJob& j, hipStream_t s) {
   }
 }
 
+// tile-shape sweep for the int8 front end (gsdrxFirFCInt8Variant): the shapes of launch_d4_complex
+// whose staging is generic over the input type
+inline hipError_t launch_d4_int8(const FirJob& j, hipStream_t s) {
+  switch (j.variant) {
+    case 0:
+      return launch_poly<float, Iq8, 4, 4, 16, 256, kModeFir, 0, true>(j, s);
+    case 1:
+      return launch_poly<float, Iq8, 4, 8, 16, 128, kModeFir, 0, true>(j, s);
+    case 3:
+      return launch_poly<float, Iq8, 4, 8, 16, 64, kModeFir, 0, true>(j, s);
+    case 4:
+      return launch_poly<float, Iq8, 4, 8, 32, 128, kModeFir, 0, true>(j, s);
+    case 5:
+      return launch_poly<float, Iq8, 4, 4, 8, 256, kModeFir, 0, true>(j, s);
+    case 24:
+      return launch_poly<float, Iq8, 4, 4, 16, 64, kModeFir, 0, true>(j, s);
+    case 27:
+      return launch_poly<float, Iq8, 4, 8, 16, 64, kModeFir, 0, true>(j, s);
+    case 28:
+      return launch_poly<float, Iq8, 4, 4, 16, 128, kModeFir, 0, true>(j, s);
+    case 50:
+      return launch_poly_cs<float, Iq8, 4, 8, 16, 256, 2, true>(j, s);
+    case 56:
+      return launch_poly_cs<float, Iq8, 4, 4, 16, 256, 2, true>(j, s);
+    case 57:
+      return launch_poly_cs<float, Iq8, 4, 8, 16, 128, 2, true>(j, s);
+    default:
+      return launch_generic<float, Iq8, kModeFir>(j, s);
+  }
+}
+
 template <class TapT, class InT, int MODE>
 hipError_t launch_fir(const FirJob& j, hipStream_t s) {
   constexpr bool kComplexIn = SampleT<InT>::kPerGranule == 2;
   // the tiled kernels address taps through a 32-bit buffer descriptor
   if (j.T > (1u << 26)) return launch_generic<TapT, InT, MODE>(j, s);
-  if constexpr (kComplexIn) {
+  if constexpr (std::is_same<InT, Iq8>::value) {
+    // int8 I/Q: the polyphase kernel (even D keeps every staged dword 4-byte aligned), else generic
+    if constexpr (MODE == kModeFir) {
+      if (j.D == 4 && j.variant >= 0) return launch_d4_int8(j, s);
+    }
+    switch (j.D) {
+      case 2:
+        return launch_poly<TapT, InT, 2, 8, 16, 128, MODE, 0, true>(j, s);
+      case 4:
+        return launch_poly<TapT, InT, 4, 4, 16, 256, MODE, 0, true>(j, s);
+      case 8:
+        return launch_poly<TapT, InT, 8, 8, 8, 128, MODE, 0, true>(j, s);
+      default:
+        return launch_generic<TapT, InT, MODE>(j, s);
+    }
+  } else if constexpr (kComplexIn) {
     switch (j.D) {
       case 1:
         return launch_contig<TapT, InT, 1, 8, 16, 256, MODE>(j, s);

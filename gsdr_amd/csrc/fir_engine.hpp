@@ -26,21 +26,68 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace gsdr {
 
 // ------------------------------------------------------------------------------------------------
 // Sample and product types
 // ------------------------------------------------------------------------------------------------
+// Interleaved int8 I/Q (2 bytes per sample, the SDR front-end format): converted to float while
+// staging with gsdrInt8ToNormFloat's semantics (reference src/conversion.cu:26), so the float
+// samples exist only in LDS.
+struct Iq8 {
+  int8_t x, y;
+};
+
+// kPerGranule: samples per 16-byte LDS granule. kSrcAlign: bytes one staging load moves from HBM
+// per granule (the alignment the vector path needs).
 template <class T>
 struct SampleT;
 template <>
 struct SampleT<float> {
   static constexpr int kPerGranule = 4;
+  static constexpr int kSrcAlign = 16;
 };
 template <>
 struct SampleT<float2> {
   static constexpr int kPerGranule = 2;
+  static constexpr int kSrcAlign = 16;
 };
+template <>
+struct SampleT<Iq8> {
+  static constexpr int kPerGranule = 2;
+  static constexpr int kSrcAlign = 4;
+};
+
+// sample type as held in LDS (what the compute core reads)
+template <class T>
+struct LdsSample {
+  using type = T;
+};
+template <>
+struct LdsSample<Iq8> {
+  using type = float2;
+};
+
+// max(-1, v / 127.0f) with IEEE division, from one multiply and an fma correction: equal to the
+// correctly rounded quotient for every int8 value (checked exhaustively, tests/test_gpu_int8.py);
+// clamping to -127 first gives the reference's max(-1, .) for -128.
+__device__ __forceinline__ float norm_i8(int v) {
+  const float x = (float)max(v, -127);
+  constexpr float r = 1.0f / 127.0f;
+  const float q = x * r;
+  return fmaf(fmaf(-q, 127.0f, x), r, q);
+}
+__device__ __forceinline__ float2 to_lds_sample(Iq8 v) { return make_float2(norm_i8(v.x), norm_i8(v.y)); }
+__device__ __forceinline__ float2 to_lds_sample(float2 v) { return v; }
+__device__ __forceinline__ float to_lds_sample(float v) { return v; }
+
+// two Iq8 samples packed in a dword -> one LDS granule
+__device__ __forceinline__ float4 iq8x2_granule(uint32_t w) {
+  const int b0 = (int)(w << 24) >> 24, b1 = (int)(w << 16) >> 24, b2 = (int)(w << 8) >> 24, b3 = (int)w >> 24;
+  return make_float4(norm_i8(b0), norm_i8(b1), norm_i8(b2), norm_i8(b3));
+}
 
 template <class TapT, class InT>
 struct Product {
@@ -197,7 +244,13 @@ __device__ __forceinline__ float4 load16_nt(const float4* p) {
 template <class InT, bool VEC>
 __device__ __forceinline__ float4 load_granule(const InT* __restrict__ in, uint64_t s, uint64_t L) {
   constexpr int G = SampleT<InT>::kPerGranule;
-  if (VEC && s + G <= L) {
+  if constexpr (std::is_same<InT, Iq8>::value) {
+    if (VEC && s + 2 <= L) return iq8x2_granule(*reinterpret_cast<const uint32_t*>(in + s));
+    float2 a = make_float2(0.0f, 0.0f), b = a;
+    if (s < L) a = to_lds_sample(in[s]);
+    if (s + 1 < L) b = to_lds_sample(in[s + 1]);
+    return make_float4(a.x, a.y, b.x, b.y);
+  } else if (VEC && s + G <= L) {
     return *reinterpret_cast<const float4*>(in + s);
   }
   float4 r = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -266,13 +319,24 @@ __device__ __forceinline__ void stage_tile(float4* __restrict__ lds, const InT* 
   for (int b0 = 0; b0 < BPT; b0 += SB) {
     float4 v[SB];
     if (whole) {
-      const float4* __restrict__ src = reinterpret_cast<const float4*>(in + S0);
+      if constexpr (std::is_same<InT, Iq8>::value) {
+        const uint32_t* __restrict__ src = reinterpret_cast<const uint32_t*>(in + S0);
+        uint32_t w[SB];
 #pragma unroll
-      for (int k = 0; k < SB; ++k) {
-        if constexpr (NT) {
-          v[k] = load16_nt(src + (b0 + k) * WG + tid);
-        } else {
-          v[k] = src[(b0 + k) * WG + tid];
+        for (int k = 0; k < SB; ++k) {
+          w[k] = NT ? __builtin_nontemporal_load(src + (b0 + k) * WG + tid) : src[(b0 + k) * WG + tid];
+        }
+#pragma unroll
+        for (int k = 0; k < SB; ++k) v[k] = iq8x2_granule(w[k]);
+      } else {
+        const float4* __restrict__ src = reinterpret_cast<const float4*>(in + S0);
+#pragma unroll
+        for (int k = 0; k < SB; ++k) {
+          if constexpr (NT) {
+            v[k] = load16_nt(src + (b0 + k) * WG + tid);
+          } else {
+            v[k] = src[(b0 + k) * WG + tid];
+          }
         }
       }
     } else {
@@ -426,7 +490,7 @@ __device__ __forceinline__ void poly_compute(const float4* __restrict__ lds, con
 #pragma unroll
         for (int e = 0; e < G; ++e) {
 #pragma unroll
-          for (int r = 0; r < R; ++r) mac(acc[r], granule_sample<InT>(win[r + j], e), tv[j][e]);
+          for (int r = 0; r < R; ++r) mac(acc[r], granule_sample<typename LdsSample<InT>::type>(win[r + j], e), tv[j][e]);
         }
       }
     }
@@ -476,7 +540,7 @@ __global__ __launch_bounds__(WG) void k_fir_poly(FirParams p) {
   if constexpr (ABL == 1) {
     const float4 v = lds[Geo::padded(threadIdx.x * Geo::SG)];
 #pragma unroll
-    for (int r = 0; r < R; ++r) mac(acc[r], granule_sample<InT>(v, r % G), 1.0f);
+    for (int r = 0; r < R; ++r) mac(acc[r], granule_sample<typename LdsSample<InT>::type>(v, r % G), 1.0f);
   } else {
     poly_compute<TapT, InT, D, R, JC, WG, TL>(lds, p, acc, ltaps);
   }
@@ -550,7 +614,7 @@ __global__ __launch_bounds__(WG) void k_fir_poly_cs(FirParams p) {
 #pragma unroll
       for (int e = 0; e < G; ++e) {
 #pragma unroll
-        for (int r = 0; r < R; ++r) mac(acc[r], granule_sample<InT>(win[r + j], e), tv[c][j][e]);
+        for (int r = 0; r < R; ++r) mac(acc[r], granule_sample<typename LdsSample<InT>::type>(win[r + j], e), tv[c][j][e]);
       }
     }
   }
@@ -821,7 +885,7 @@ __global__ __launch_bounds__(WG) void k_fir_contig(FirParams p) {
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         const int s = r * D + i;
-        mac(acc[r], granule_sample<InT>(win[s / G], s % G), tv);
+        mac(acc[r], granule_sample<typename LdsSample<InT>::type>(win[s / G], s % G), tv);
       }
     }
   }
@@ -844,7 +908,7 @@ __device__ __forceinline__ typename Product<TapT, InT>::type fir_point(const Fir
   set_zero(acc);
   const uint64_t s0 = k * p.D;
   for (uint32_t i = 0; i < p.T; ++i) {
-    InT x = in[s0 + i];
+    auto x = to_lds_sample(in[s0 + i]);
     if constexpr (MODE != kModeFir) {
       x = nco_mix(x, p.nco_n0 + (uint32_t)(s0 + i), p.nco_inc);
     }

@@ -30,10 +30,10 @@ static bool nco_increment(float fs, float tune, float chan, uint32_t* inc) {
   return true;
 }
 
+template <class InT>
 static hipError_t chain_entry(int mode, float fs, float tune, float chan, float dev, uint32_t decimation,
-                              size_t firstSampleIndex, const float* taps, size_t tapCount,
-                              const hipFloatComplex* input, float* output, size_t numOutputs, int32_t device,
-                              hipStream_t stream) {
+                              size_t firstSampleIndex, const float* taps, size_t tapCount, const InT* input,
+                              float* output, size_t numOutputs, int32_t device, hipStream_t stream) {
   if (numOutputs == 0) return hipSuccess;
   if (decimation == 0 || output == nullptr || input == nullptr) return hipErrorInvalidValue;
   if (tapCount > 0 && taps == nullptr) return hipErrorInvalidValue;
@@ -57,11 +57,11 @@ static hipError_t chain_entry(int mode, float fs, float tune, float chan, float 
   if (scope.status() != hipSuccess) return scope.status();
   if (tapCount == 0) {
     // y == 0 everywhere: the generic kernel evaluates the epilogue on zero without touching taps
-    return mode == kModeFm ? launch_generic<float, float2, kModeFm>(job, stream)
-                           : launch_generic<float, float2, kModeAm>(job, stream);
+    return mode == kModeFm ? launch_generic<float, InT, kModeFm>(job, stream)
+                           : launch_generic<float, InT, kModeAm>(job, stream);
   }
-  return mode == kModeFm ? launch_fir<float, float2, kModeFm>(job, stream)
-                         : launch_fir<float, float2, kModeAm>(job, stream);
+  return mode == kModeFm ? launch_fir<float, InT, kModeFm>(job, stream)
+                         : launch_fir<float, InT, kModeAm>(job, stream);
 }
 
 }  // namespace gsdr
@@ -72,8 +72,8 @@ GSDR_C_LINKAGE hipError_t gsdrFmDemod(float rfSampleRate, float tuningFrequency,
                                       float* output, size_t numOutputs, int32_t cudaDevice,
                                       hipStream_t cudaStream) GSDR_NO_EXCEPT {
   return gsdr::chain_entry(gsdr::kModeFm, rfSampleRate, tuningFrequency, channelFrequency, frequencyDeviation,
-                           decimation, firstSampleIndex, lowPassTaps, numLowPassTaps, input, output, numOutputs,
-                           cudaDevice, cudaStream);
+                           decimation, firstSampleIndex, lowPassTaps, numLowPassTaps,
+                           reinterpret_cast<const float2*>(input), output, numOutputs, cudaDevice, cudaStream);
 }
 
 GSDR_C_LINKAGE hipError_t gsdrAmDemod(float rfSampleRate, float tuningFrequency, float channelFrequency,
@@ -81,8 +81,28 @@ GSDR_C_LINKAGE hipError_t gsdrAmDemod(float rfSampleRate, float tuningFrequency,
                                       size_t numLowPassTaps, const hipFloatComplex* input, float* output,
                                       size_t numElements, int32_t cudaDevice, hipStream_t cudaStream) GSDR_NO_EXCEPT {
   return gsdr::chain_entry(gsdr::kModeAm, rfSampleRate, tuningFrequency, channelFrequency, 1.0f, decimation,
-                           firstSampleIndex, lowPassTaps, numLowPassTaps, input, output, numElements, cudaDevice,
-                           cudaStream);
+                           firstSampleIndex, lowPassTaps, numLowPassTaps, reinterpret_cast<const float2*>(input),
+                           output, numElements, cudaDevice, cudaStream);
+}
+
+GSDR_C_LINKAGE hipError_t gsdrxFmDemodInt8(float rfSampleRate, float tuningFrequency, float channelFrequency,
+                                           float frequencyDeviation, uint32_t decimation, size_t firstSampleIndex,
+                                           const float* lowPassTaps, size_t numLowPassTaps, const int8_t* input,
+                                           float* output, size_t numOutputs, int32_t cudaDevice,
+                                           hipStream_t cudaStream) GSDR_NO_EXCEPT {
+  return gsdr::chain_entry(gsdr::kModeFm, rfSampleRate, tuningFrequency, channelFrequency, frequencyDeviation,
+                           decimation, firstSampleIndex, lowPassTaps, numLowPassTaps,
+                           reinterpret_cast<const gsdr::Iq8*>(input), output, numOutputs, cudaDevice, cudaStream);
+}
+
+GSDR_C_LINKAGE hipError_t gsdrxAmDemodInt8(float rfSampleRate, float tuningFrequency, float channelFrequency,
+                                           uint32_t decimation, size_t firstSampleIndex, const float* lowPassTaps,
+                                           size_t numLowPassTaps, const int8_t* input, float* output,
+                                           size_t numElements, int32_t cudaDevice,
+                                           hipStream_t cudaStream) GSDR_NO_EXCEPT {
+  return gsdr::chain_entry(gsdr::kModeAm, rfSampleRate, tuningFrequency, channelFrequency, 1.0f, decimation,
+                           firstSampleIndex, lowPassTaps, numLowPassTaps, reinterpret_cast<const gsdr::Iq8*>(input),
+                           output, numElements, cudaDevice, cudaStream);
 }
 
 GSDR_C_LINKAGE uint32_t gsdrNcoPhaseIncrement(float rfSampleRate, float tuningFrequency,

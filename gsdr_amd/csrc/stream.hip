@@ -1,0 +1,219 @@
+// gsdr-mi355x: streaming continuity object (include/gsdr/stream.h).
+//
+// Host-side bookkeeping around the filter entry points. The reference has no equivalent: its callers
+// re-supply the overlap themselves (include/gsdr/fm.h:26, fm.cu:202). Per Process call:
+//   * seam outputs (window starts in the history, ends in the new chunk): history + chunk head are
+//     stitched into a small device buffer and filtered from there;
+//   * every other computable output is filtered straight from the caller's chunk;
+//   * the samples the next output still needs (< one window) become the new history.
+// Each launch passes the absolute index of its first sample as firstSampleIndex, so the NCO phase
+// and the kernel selection are those of one monolithic call: the outputs are bit-identical.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <new>
+
+#include "gsdr/am.h"
+#include "gsdr/fir.h"
+#include "gsdr/fm.h"
+#include "gsdr/gsdr_ext.h"
+#include "gsdr/stream.h"
+#include "launch.hpp"
+
+struct gsdrxStream_t {
+  int kind = GSDRX_STREAM_FIR;
+  int format = GSDRX_SAMPLES_CF32;
+  uint32_t D = 1;
+  const float* taps = nullptr;
+  size_t T = 0;
+  size_t W = 0;  // samples one output needs
+  float fs = 0.0f, tune = 0.0f, chan = 0.0f, dev = 0.0f;
+  uint64_t n0 = 0;  // absolute index of stream sample 0
+  int32_t device = 0;
+  size_t sb = 8;  // bytes per input sample
+  size_t ob = 8;  // bytes per output
+  uint64_t consumed = 0;
+  uint64_t next_out = 0;
+  char* hist = nullptr;   // samples [next_out * D, consumed) (empty if next_out * D >= consumed)
+  char* spare = nullptr;  // the other history buffer (ping-pong)
+  char* seam = nullptr;   // history + chunk head for the seam outputs
+};
+
+namespace gsdr {
+namespace {
+
+struct Plan {
+  uint64_t n_seam, head, n_main, main_off, hist_after, m_mid, m_end;
+};
+
+Plan make_plan(uint32_t D, uint64_t W, uint64_t S, uint64_t m_next, uint64_t M) {
+  Plan p{};
+  const uint64_t S_new = S + M;
+  uint64_t m_end = S_new >= W ? (S_new - W) / D + 1 : 0;  // first output whose window is incomplete
+  m_end = std::max(m_end, m_next);
+  const uint64_t m_mid = std::min(std::max(ceil_div<uint64_t>(S, D), m_next), m_end);
+  p.m_mid = m_mid;
+  p.m_end = m_end;
+  p.n_seam = m_mid - m_next;
+  p.head = p.n_seam ? (m_mid - 1) * D + W - S : 0;  // chunk samples the last seam output reads
+  p.n_main = m_end - m_mid;
+  p.main_off = p.n_main ? m_mid * D - S : 0;
+  const uint64_t from = m_end * D;
+  p.hist_after = S_new > from ? S_new - from : 0;
+  return p;
+}
+
+hipError_t filter(const gsdrxStream_t& s, const void* in, uint64_t first, void* out, size_t n, hipStream_t st) {
+  const bool i8 = s.format == GSDRX_SAMPLES_CS8;
+  switch (s.kind) {
+    case GSDRX_STREAM_FIR:
+      return i8 ? gsdrxFirFCInt8(s.D, s.taps, s.T, static_cast<const int8_t*>(in), static_cast<hipFloatComplex*>(out),
+                                 n, s.device, st)
+                : gsdrFirFC(s.D, s.taps, s.T, static_cast<const hipFloatComplex*>(in),
+                            static_cast<hipFloatComplex*>(out), n, s.device, st);
+    case GSDRX_STREAM_FM:
+      return i8 ? gsdrxFmDemodInt8(s.fs, s.tune, s.chan, s.dev, s.D, first, s.taps, s.T,
+                                   static_cast<const int8_t*>(in), static_cast<float*>(out), n, s.device, st)
+                : gsdrFmDemod(s.fs, s.tune, s.chan, s.dev, s.D, first, s.taps, s.T,
+                              static_cast<const hipFloatComplex*>(in), static_cast<float*>(out), n, s.device, st);
+    default:
+      return i8 ? gsdrxAmDemodInt8(s.fs, s.tune, s.chan, s.D, first, s.taps, s.T, static_cast<const int8_t*>(in),
+                                   static_cast<float*>(out), n, s.device, st)
+                : gsdrAmDemod(s.fs, s.tune, s.chan, s.D, first, s.taps, s.T, static_cast<const hipFloatComplex*>(in),
+                              static_cast<float*>(out), n, s.device, st);
+  }
+}
+
+hipError_t copy(void* dst, const void* src, size_t bytes, hipStream_t st) {
+  return bytes ? hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st) : hipSuccess;
+}
+
+}  // namespace
+}  // namespace gsdr
+
+using gsdr::Plan;
+
+GSDR_C_LINKAGE void gsdrxStreamPlan(uint32_t decimation, size_t window, uint64_t consumed, uint64_t nextOutput,
+                                    size_t chunk, uint64_t plan[5]) GSDR_NO_EXCEPT {
+  if (plan == nullptr) return;
+  if (decimation == 0 || window == 0) {
+    for (int i = 0; i < 5; ++i) plan[i] = 0;
+    return;
+  }
+  const Plan p = gsdr::make_plan(decimation, window, consumed, nextOutput, chunk);
+  plan[0] = p.n_seam;
+  plan[1] = p.head;
+  plan[2] = p.n_main;
+  plan[3] = p.main_off;
+  plan[4] = p.hist_after;
+}
+
+GSDR_C_LINKAGE hipError_t gsdrxStreamCreate(gsdrxStream* stream, int kind, int sampleFormat, uint32_t decimation,
+                                            const float* taps, size_t tapCount, float rfSampleRate,
+                                            float tuningFrequency, float channelFrequency, float frequencyDeviation,
+                                            size_t firstSampleIndex, int32_t cudaDevice) GSDR_NO_EXCEPT {
+  if (stream == nullptr) return hipErrorInvalidValue;
+  *stream = nullptr;
+  if (decimation == 0 || tapCount == 0 || taps == nullptr) return hipErrorInvalidValue;
+  if (kind != GSDRX_STREAM_FIR && kind != GSDRX_STREAM_FM && kind != GSDRX_STREAM_AM) return hipErrorInvalidValue;
+  if (sampleFormat != GSDRX_SAMPLES_CF32 && sampleFormat != GSDRX_SAMPLES_CS8) return hipErrorInvalidValue;
+  gsdrxStream s = new (std::nothrow) gsdrxStream_t;
+  if (s == nullptr) return hipErrorOutOfMemory;
+  s->kind = kind;
+  s->format = sampleFormat;
+  s->D = decimation;
+  s->taps = taps;
+  s->T = tapCount;
+  s->W = kind == GSDRX_STREAM_FM ? tapCount + decimation : tapCount;
+  s->fs = rfSampleRate;
+  s->tune = tuningFrequency;
+  s->chan = channelFrequency;
+  s->dev = frequencyDeviation;
+  s->n0 = firstSampleIndex;
+  s->device = cudaDevice;
+  s->sb = sampleFormat == GSDRX_SAMPLES_CS8 ? 2 : 8;
+  s->ob = kind == GSDRX_STREAM_FIR ? 8 : 4;
+  gsdr::DeviceScope scope(cudaDevice);
+  hipError_t e = scope.status();
+  const size_t hist_bytes = s->W * s->sb;  // history < W samples
+  const size_t seam_bytes = 2 * s->W * s->sb;
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s->hist), hist_bytes);
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s->spare), hist_bytes);
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s->seam), seam_bytes);
+  if (e != hipSuccess) {
+    (void)gsdrxStreamDestroy(s);
+    return e;
+  }
+  *stream = s;
+  return hipSuccess;
+}
+
+GSDR_C_LINKAGE size_t gsdrxStreamOutputsFor(gsdrxStream s, size_t numInputSamples) GSDR_NO_EXCEPT {
+  if (s == nullptr) return 0;
+  const Plan p = gsdr::make_plan(s->D, s->W, s->consumed, s->next_out, numInputSamples);
+  return p.n_seam + p.n_main;
+}
+
+GSDR_C_LINKAGE hipError_t gsdrxStreamProcess(gsdrxStream s, const void* input, size_t numInputSamples, void* output,
+                                             size_t outputCapacity, size_t* numOutputsWritten,
+                                             hipStream_t cudaStream) GSDR_NO_EXCEPT {
+  if (numOutputsWritten) *numOutputsWritten = 0;
+  if (s == nullptr) return hipErrorInvalidValue;
+  if (numInputSamples == 0) return hipSuccess;
+  if (input == nullptr) return hipErrorInvalidValue;
+  const Plan p = gsdr::make_plan(s->D, s->W, s->consumed, s->next_out, numInputSamples);
+  const size_t n_out = p.n_seam + p.n_main;
+  if (n_out > outputCapacity || (n_out && output == nullptr)) return hipErrorInvalidValue;
+  gsdr::DeviceScope scope(s->device);
+  if (scope.status() != hipSuccess) return scope.status();
+  const char* chunk = static_cast<const char*>(input);
+  char* out = static_cast<char*>(output);
+  const uint64_t S = s->consumed, h0 = s->next_out * s->D;
+  const uint64_t h = S > h0 ? S - h0 : 0;
+  hipError_t e = hipSuccess;
+  if (p.n_seam) {
+    e = gsdr::copy(s->seam, s->hist, h * s->sb, cudaStream);
+    if (e == hipSuccess) e = gsdr::copy(s->seam + h * s->sb, chunk, p.head * s->sb, cudaStream);
+    if (e == hipSuccess) e = gsdr::filter(*s, s->seam, s->n0 + h0, out, p.n_seam, cudaStream);
+  }
+  if (e == hipSuccess && p.n_main) {
+    e = gsdr::filter(*s, chunk + p.main_off * s->sb, s->n0 + p.m_mid * s->D, out + p.n_seam * s->ob, p.n_main,
+                     cudaStream);
+  }
+  if (e == hipSuccess && p.hist_after) {
+    const uint64_t from = p.m_end * s->D, S_new = S + numInputSamples;
+    uint64_t done = 0;
+    if (from < S) {  // part of the new history is still in the old one
+      done = S - from;
+      e = gsdr::copy(s->spare, s->hist + (from - h0) * s->sb, done * s->sb, cudaStream);
+    }
+    const uint64_t c0 = from > S ? from - S : 0;
+    if (e == hipSuccess) e = gsdr::copy(s->spare + done * s->sb, chunk + c0 * s->sb, (S_new - S - c0) * s->sb, cudaStream);
+    std::swap(s->hist, s->spare);
+  }
+  if (e != hipSuccess) return e;
+  s->consumed += numInputSamples;
+  s->next_out = p.m_end;
+  if (numOutputsWritten) *numOutputsWritten = n_out;
+  return hipSuccess;
+}
+
+GSDR_C_LINKAGE hipError_t gsdrxStreamDestroy(gsdrxStream s) GSDR_NO_EXCEPT {
+  if (s == nullptr) return hipSuccess;
+  hipError_t e = hipSuccess;
+  {
+    gsdr::DeviceScope scope(s->device);
+    if (scope.status() == hipSuccess) {
+      for (char* b : {s->hist, s->spare, s->seam}) {
+        if (b) {
+          const hipError_t f = hipFree(b);
+          if (e == hipSuccess) e = f;
+        }
+      }
+    } else {
+      e = scope.status();
+    }
+  }
+  delete s;
+  return e;
+}

@@ -49,7 +49,21 @@ _FIR = {
     (torch.float32, torch.float32): ("gsdrFirFF", torch.float32),
     (torch.complex64, torch.complex64): ("gsdrFirCC", torch.complex64),
     (torch.complex64, torch.float32): ("gsdrFirCF", torch.complex64),
+    (torch.float32, torch.int8): ("gsdrxFirFCInt8", torch.complex64),  # interleaved int8 I/Q
 }
+
+
+def _nsamp(x):
+    """samples in x: int8 tensors hold interleaved I/Q pairs (gsdr_ext.h)."""
+    if x.dtype == torch.int8:
+        if x.numel() % 2:
+            raise ValueError("int8 I/Q input needs an even number of elements")
+        return x.numel() // 2
+    return x.numel()
+
+
+def _require_samples(x, dtype, name, min_samples):
+    _require(x, dtype, name, min_samples * (2 if dtype == torch.int8 else 1))
 
 
 def _fir_prepare(taps, x, decimation, num_outputs, out):
@@ -58,10 +72,11 @@ def _fir_prepare(taps, x, decimation, num_outputs, out):
         raise TypeError(f"unsupported tap/input dtypes {key}")
     name, odt = _FIR[key]
     T = taps.numel()
+    L = _nsamp(x)
     if num_outputs is None:
-        num_outputs = (x.numel() - T) // decimation + 1 if x.numel() >= T else 0
+        num_outputs = (L - T) // decimation + 1 if L >= T else 0
     if num_outputs > 0:
-        _require(x, x.dtype, "input", (num_outputs - 1) * decimation + T)
+        _require_samples(x, x.dtype, "input", (num_outputs - 1) * decimation + T)
     if out is None:
         out = torch.empty(num_outputs, dtype=odt, device=x.device)
     _require(out, odt, "output", num_outputs)
@@ -90,18 +105,22 @@ def fir_variant(variant: int, taps: torch.Tensor, x: torch.Tensor, decimation: i
 
 def fm_demod(x, taps, rf_sample_rate, tuning_frequency, channel_frequency, frequency_deviation, decimation,
              first_sample_index=0, num_outputs=None, out=None):
-    """gsdrFmDemod: NCO shift + low-pass FIR + decimation + FM discriminator (fm.h)."""
-    _require(x, torch.complex64, "input")
+    """gsdrFmDemod: NCO shift + low-pass FIR + decimation + FM discriminator (fm.h); int8 I/Q input
+    selects gsdrxFmDemodInt8."""
+    if x.dtype not in (torch.complex64, torch.int8):
+        raise TypeError(f"input: expected complex64 or int8 I/Q, got {x.dtype}")
+    _require(x, x.dtype, "input")
     _require(taps, torch.float32, "taps")
     T = taps.numel()
     if num_outputs is None:
-        num_outputs = max(0, (x.numel() - T) // decimation)
+        num_outputs = max(0, (_nsamp(x) - T) // decimation)
     if num_outputs > 0:
-        _require(x, torch.complex64, "input", num_outputs * decimation + T)
+        _require_samples(x, x.dtype, "input", num_outputs * decimation + T)
     if out is None:
         out = torch.empty(num_outputs, dtype=torch.float32, device=x.device)
     _require(out, torch.float32, "output", num_outputs)
-    check("gsdrFmDemod", lib.gsdrFmDemod(rf_sample_rate, tuning_frequency, channel_frequency, frequency_deviation,
+    name = "gsdrxFmDemodInt8" if x.dtype == torch.int8 else "gsdrFmDemod"
+    check(name, getattr(lib, name)(rf_sample_rate, tuning_frequency, channel_frequency, frequency_deviation,
                                          decimation, first_sample_index, _ptr(taps), T, _ptr(x), _ptr(out),
                                          num_outputs, _dev(x), stream_of(x)))
     return out
@@ -109,18 +128,23 @@ def fm_demod(x, taps, rf_sample_rate, tuning_frequency, channel_frequency, frequ
 
 def am_demod(x, taps, rf_sample_rate, tuning_frequency, channel_frequency, decimation, first_sample_index=0,
              num_outputs=None, out=None):
-    """gsdrAmDemod: NCO shift + low-pass FIR + decimation + envelope (am.h)."""
-    _require(x, torch.complex64, "input")
+    """gsdrAmDemod: NCO shift + low-pass FIR + decimation + envelope (am.h); int8 I/Q input selects
+    gsdrxAmDemodInt8."""
+    if x.dtype not in (torch.complex64, torch.int8):
+        raise TypeError(f"input: expected complex64 or int8 I/Q, got {x.dtype}")
+    _require(x, x.dtype, "input")
     _require(taps, torch.float32, "taps")
     T = taps.numel()
+    L = _nsamp(x)
     if num_outputs is None:
-        num_outputs = (x.numel() - T) // decimation + 1 if x.numel() >= T else 0
+        num_outputs = (L - T) // decimation + 1 if L >= T else 0
     if num_outputs > 0:
-        _require(x, torch.complex64, "input", (num_outputs - 1) * decimation + T)
+        _require_samples(x, x.dtype, "input", (num_outputs - 1) * decimation + T)
     if out is None:
         out = torch.empty(num_outputs, dtype=torch.float32, device=x.device)
     _require(out, torch.float32, "output", num_outputs)
-    check("gsdrAmDemod", lib.gsdrAmDemod(rf_sample_rate, tuning_frequency, channel_frequency, decimation,
+    name = "gsdrxAmDemodInt8" if x.dtype == torch.int8 else "gsdrAmDemod"
+    check(name, getattr(lib, name)(rf_sample_rate, tuning_frequency, channel_frequency, decimation,
                                          first_sample_index, _ptr(taps), T, _ptr(x), _ptr(out), num_outputs,
                                          _dev(x), stream_of(x)))
     return out

@@ -1,0 +1,77 @@
+"""torch view of the streaming continuity object (include/gsdr/stream.h).
+
+    s = Stream("fm", taps, decimation=4, rf_sample_rate=1e6, channel_frequency=1e5,
+               frequency_deviation=2e4)
+    for chunk in chunks:            # complex64 (or int8 I/Q) device tensors of any length
+        audio = s.process(chunk)    # every output that became computable, in order
+
+Concatenated over the calls, the outputs equal one gsdrFirFC / gsdrFmDemod / gsdrAmDemod call over
+the concatenated input, bit for bit.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from .abi import GsdrError, check, lib
+from .ops import stream_of
+
+KINDS = {"fir": 0, "fm": 1, "am": 2}
+
+
+class Stream:
+    def __init__(self, kind: str, taps: torch.Tensor, decimation: int, rf_sample_rate: float = 1.0,
+                 tuning_frequency: float = 0.0, channel_frequency: float = 0.0, frequency_deviation: float = 1.0,
+                 first_sample_index: int = 0, int8: bool = False):
+        if kind not in KINDS:
+            raise ValueError(f"kind must be one of {sorted(KINDS)}")
+        if taps.dtype != torch.float32 or taps.device.type != "cuda" or not taps.is_contiguous():
+            raise TypeError("taps must be a contiguous float32 device tensor")
+        self.kind, self.int8, self.taps = kind, int8, taps  # keep taps alive: the stream reads them
+        self.device = taps.device
+        self._h = ctypes.c_void_p()
+        check("gsdrxStreamCreate", lib.gsdrxStreamCreate(
+            ctypes.byref(self._h), KINDS[kind], 1 if int8 else 0, decimation, taps.data_ptr(), taps.numel(),
+            rf_sample_rate, tuning_frequency, channel_frequency, frequency_deviation, first_sample_index,
+            self.device.index))
+
+    def outputs_for(self, num_samples: int) -> int:
+        return lib.gsdrxStreamOutputsFor(self._h, num_samples)
+
+    def process(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        want = torch.int8 if self.int8 else torch.complex64
+        if x.dtype != want or not x.is_contiguous() or x.device != self.device:
+            raise TypeError(f"input must be a contiguous {want} tensor on {self.device}")
+        n_in = x.numel() // 2 if self.int8 else x.numel()
+        n_out = self.outputs_for(n_in)
+        odt = torch.complex64 if self.kind == "fir" else torch.float32
+        if out is None:
+            out = torch.empty(n_out, dtype=odt, device=self.device)
+        if out.dtype != odt or out.numel() < n_out:
+            raise ValueError(f"output must hold {n_out} {odt} values")
+        written = ctypes.c_size_t(0)
+        check("gsdrxStreamProcess", lib.gsdrxStreamProcess(self._h, x.data_ptr() if n_in else None, n_in,
+                                                           out.data_ptr() if n_out else None, out.numel(),
+                                                           ctypes.byref(written), stream_of(x)))
+        if written.value != n_out:
+            raise GsdrError("gsdrxStreamProcess", -1)
+        return out[:n_out]
+
+    def close(self):
+        if self._h:
+            check("gsdrxStreamDestroy", lib.gsdrxStreamDestroy(self._h))
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def plan(decimation: int, window: int, consumed: int, next_output: int, chunk: int):
+    """gsdrxStreamPlan: (seam outputs, chunk head copied, direct outputs, direct offset, history after)."""
+    out = (ctypes.c_uint64 * 5)()
+    lib.gsdrxStreamPlan(decimation, window, consumed, next_output, chunk, out)
+    return tuple(int(v) for v in out)

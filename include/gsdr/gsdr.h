@@ -14,6 +14,7 @@
 #include <gsdr/qpsk.h>
 #include <gsdr/qpsk256.h>
 #include <gsdr/quad_demod.h>
+#include <gsdr/stream.h>
 #include <gsdr/trig.h>
 #include <gsdr/util.h>
 

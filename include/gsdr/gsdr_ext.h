@@ -42,4 +42,67 @@ GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxFirFCVariant(
     int32_t cudaDevice,
     hipStream_t cudaStream) GSDR_NO_EXCEPT;
 
+/*
+ * int8 I/Q front end fused into the filters. `input` holds interleaved
+ * int8 I/Q pairs (2 bytes per complex sample; sample counts as in the float entry points). Each
+ * component is converted exactly as gsdrInt8ToNormFloat does (max(-1, v / 127.0f), reference
+ * src/conversion.cu:26) while the tile is staged, so the results are bit-identical to running
+ * gsdrInt8ToNormFloat over the 2*L components and then the float entry point with the same
+ * arguments -- without the float intermediate in HBM (2 instead of 8 input bytes per sample).
+ */
+
+/** gsdrFirFC (fir.h) on int8 I/Q input. */
+GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxFirFCInt8(
+    size_t decimation,
+    const float* taps,
+    size_t tapCount,
+    const int8_t* input,
+    hipFloatComplex* output,
+    size_t numOutputs,
+    int32_t cudaDevice,
+    hipStream_t cudaStream) GSDR_NO_EXCEPT;
+
+/** gsdrxFirFCInt8 with an explicit decimation-4 tile shape (tuning sweep; -1 = default). */
+GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxFirFCInt8Variant(
+    int variant,
+    size_t decimation,
+    const float* taps,
+    size_t tapCount,
+    const int8_t* input,
+    hipFloatComplex* output,
+    size_t numOutputs,
+    int32_t cudaDevice,
+    hipStream_t cudaStream) GSDR_NO_EXCEPT;
+
+/** gsdrFmDemod (fm.h) on int8 I/Q input. */
+GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxFmDemodInt8(
+    float rfSampleRate,
+    float tuningFrequency,
+    float channelFrequency,
+    float frequencyDeviation,
+    uint32_t decimation,
+    size_t firstSampleIndex,
+    const float* lowPassTaps,
+    size_t numLowPassTaps,
+    const int8_t* input,
+    float* output,
+    size_t numOutputs,
+    int32_t cudaDevice,
+    hipStream_t cudaStream) GSDR_NO_EXCEPT;
+
+/** gsdrAmDemod (am.h) on int8 I/Q input. */
+GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxAmDemodInt8(
+    float rfSampleRate,
+    float tuningFrequency,
+    float channelFrequency,
+    uint32_t decimation,
+    size_t firstSampleIndex,
+    const float* lowPassTaps,
+    size_t numLowPassTaps,
+    const int8_t* input,
+    float* output,
+    size_t numElements,
+    int32_t cudaDevice,
+    hipStream_t cudaStream) GSDR_NO_EXCEPT;
+
 #endif /* GSDR_EXT_H_ */

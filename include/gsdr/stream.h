@@ -1,0 +1,104 @@
+/*
+ * gsdr-mi355x extension: streaming continuity.
+ *
+ * The reference leaves the overlap between consecutive calls to the caller (include/gsdr/fm.h:26,
+ * `firstSampleIndex` fm.h:48, am.h:30, fm.cu:202): to filter a stream in chunks, the caller must
+ * re-supply the last taps-1 samples of the previous chunk and advance the NCO index itself. A
+ * gsdrxStream object does that bookkeeping on the device: it keeps the samples the next output still
+ * needs (fewer than one filter window) in a small device buffer, computes the outputs whose window
+ * straddles the seam from that history plus the head of the new chunk, computes every other output
+ * directly from the caller's chunk, and advances the absolute sample index that the NCO phase is
+ * derived from.
+ *
+ * Contract: feeding a signal x[0..S) in chunks of any sizes (including 0 and chunks shorter than the
+ * filter) produces, concatenated over the calls, exactly the outputs of ONE call of the underlying
+ * entry point over x[0..S) with firstSampleIndex = the value given at creation -- bit for bit
+ * (the seam and main launches use the same kernels as the single call, and the NCO phase is a
+ * function of the absolute sample index). Output m is produced by the first call after which its
+ * whole window has arrived: FIR/AM windows are taps samples, FM windows taps + decimation samples.
+ *
+ * Kinds: GSDRX_STREAM_FIR (gsdrFirFC), GSDRX_STREAM_FM (gsdrFmDemod), GSDRX_STREAM_AM (gsdrAmDemod).
+ * Sample formats: GSDRX_SAMPLES_CF32 (hipFloatComplex) or GSDRX_SAMPLES_CS8 (interleaved int8 I/Q,
+ * the gsdrx*Int8 entry points of gsdr_ext.h).
+ *
+ * Threading: one object is one stream; calls on it must be ordered (same hipStream_t, or the caller
+ * orders them). The taps buffer is the caller's and must stay valid while the object is used.
+ */
+#ifndef GSDR_STREAM_H_
+#define GSDR_STREAM_H_
+
+#include <gsdr/gsdr_export.h>
+#include <gsdr/util.h>
+#include <hip/hip_runtime_api.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#define GSDRX_STREAM_FIR 0
+#define GSDRX_STREAM_FM 1
+#define GSDRX_STREAM_AM 2
+
+#define GSDRX_SAMPLES_CF32 0
+#define GSDRX_SAMPLES_CS8 1
+
+typedef struct gsdrxStream_t* gsdrxStream;
+
+/**
+ * Create a stream on `cudaDevice` (allocates two history buffers and a seam buffer of at most
+ * 2 * (tapCount + decimation) samples each; nothing is allocated later). For GSDRX_STREAM_FIR the
+ * frequency arguments are ignored; for GSDRX_STREAM_AM frequencyDeviation is ignored.
+ * Returns hipErrorInvalidValue for a null handle pointer, decimation == 0, tapCount == 0, null taps
+ * or an unknown kind / sample format.
+ */
+GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxStreamCreate(
+    gsdrxStream* stream,
+    int kind,
+    int sampleFormat,
+    uint32_t decimation,
+    const float* taps,
+    size_t tapCount,
+    float rfSampleRate,
+    float tuningFrequency,
+    float channelFrequency,
+    float frequencyDeviation,
+    size_t firstSampleIndex,
+    int32_t cudaDevice) GSDR_NO_EXCEPT;
+
+/** Number of outputs the next gsdrxStreamProcess call with `numInputSamples` samples will write. */
+GSDR_C_LINKAGE GSDR_PUBLIC size_t gsdrxStreamOutputsFor(gsdrxStream stream, size_t numInputSamples) GSDR_NO_EXCEPT;
+
+/**
+ * Append `numInputSamples` samples (device memory, in the stream's sample format) and write every
+ * output that became computable to `output` (hipFloatComplex for FIR, float for FM/AM), in order.
+ * `*numOutputsWritten` receives the count (host-known, no synchronisation). Asynchronous on
+ * `cudaStream`; the input chunk may be reused once the stream's work has completed. Returns
+ * hipErrorInvalidValue, leaving the stream unchanged, when outputCapacity is too small.
+ */
+GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxStreamProcess(
+    gsdrxStream stream,
+    const void* input,
+    size_t numInputSamples,
+    void* output,
+    size_t outputCapacity,
+    size_t* numOutputsWritten,
+    hipStream_t cudaStream) GSDR_NO_EXCEPT;
+
+/** Free the stream's device buffers (synchronises the device, as hipFree does). Null is a no-op. */
+GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxStreamDestroy(gsdrxStream stream) GSDR_NO_EXCEPT;
+
+/**
+ * The host-side plan of one Process call, exposed so the planning logic can be tested without a GPU.
+ * Inputs: decimation D, window W (samples one output needs), samples consumed so far, index of the
+ * next output, chunk length. plan[0] = seam outputs (computed from history + chunk head),
+ * plan[1] = samples of the chunk head copied behind the history for them, plan[2] = outputs computed
+ * directly from the chunk, plan[3] = chunk offset of the first direct output's window,
+ * plan[4] = history length after the call.
+ */
+GSDR_C_LINKAGE GSDR_PUBLIC void gsdrxStreamPlan(
+    uint32_t decimation,
+    size_t window,
+    uint64_t consumed,
+    uint64_t nextOutput,
+    size_t chunk,
+    uint64_t plan[5]) GSDR_NO_EXCEPT;
+
+#endif /* GSDR_STREAM_H_ */

@@ -24,14 +24,20 @@ ap.add_argument("--variants", default="0,1,107,111")
 ap.add_argument("--launches", type=int, default=400)
 ap.add_argument("--window", type=int, default=50)
 ap.add_argument("--cool", type=float, default=2.0, help="idle seconds before each variant")
+ap.add_argument("--int8", action="store_true", help="int8 I/Q input (gsdrxFirFCInt8Variant)")
 a = ap.parse_args()
+if a.int8:
+    BYTES = 2 * L + 8 * N + 4 * TAPS
 dev = torch.device("cuda", 0)
 g = torch.Generator(device=dev).manual_seed(0x5EED)
-xs = [(torch.rand(2 * L, device=dev, generator=g) * 2 - 1).view(torch.complex64) for _ in range(3)]
+if a.int8:
+    xs = [torch.randint(-128, 128, (2 * L,), dtype=torch.int8, device=dev, generator=g) for _ in range(3)]
+else:
+    xs = [(torch.rand(2 * L, device=dev, generator=g) * 2 - 1).view(torch.complex64) for _ in range(3)]
 taps = torch.from_numpy(lowpass_taps(TAPS)).to(dev)
 y = torch.empty(N, dtype=torch.complex64, device=dev)
 stream = torch.cuda.current_stream(dev).cuda_stream
-fn = abi.lib.gsdrxFirFCVariant
+fn = abi.lib.gsdrxFirFCInt8Variant if a.int8 else abi.lib.gsdrxFirFCVariant
 for v in [int(s) for s in a.variants.split(",")]:
     argsets = [(v, D, taps.data_ptr(), TAPS, x.data_ptr(), y.data_ptr(), N, 0, stream) for x in xs]
     torch.cuda.synchronize()

@@ -174,6 +174,8 @@ def secondary_configs(torch, ops, device, taps):
     """Config 3 (fused NCO + FIR + FM, 64 M samples), the int8 I/Q front end on
     the config-2 and config-3 shapes, and config 5 (QPSK256 16 M symbols): kernel times from HIP
     events, reported beside the headline line."""
+    import ctypes
+
     import numpy as np
 
     from gsdr_amd import abi
@@ -193,6 +195,20 @@ def secondary_configs(torch, ops, device, taps):
     out["fm_chain"] = {"config": "NCO + 127-tap FIR (D=4) + FM discriminator, 67,108,987 samples (BASELINE configs[2])",
                        "us_per_launch": round(t * 1e6, 2), "msamples_per_s": round(n_in / t / 1e6, 1),
                        "alg_gbps": round(b / t / 1e9, 1), "alg_bytes_per_launch": b}
+    # multi-channel chain: C channels from one read of the input
+    for C in (4, 16):
+        chans = (ctypes.c_float * C)(*[float(f) for f in np.linspace(-0.4, 0.4, C) * fs])
+        devs = (ctypes.c_float * C)(*([dev_hz] * C))
+        ym = torch.empty(C * n_fm, dtype=torch.float32, device=device)
+        argsets = [(fs, tune, chans, devs, C, DECIM, 0, taps.data_ptr(), TAPS, 0, x.data_ptr(), ym.data_ptr(), n_fm,
+                    device.index, stream) for x in xs]
+        t = time_abi(torch, abi.lib.gsdrxFmDemodMulti, argsets, reps=20)
+        out[f"fm_multi_{C}ch"] = {
+            "config": f"{C} FM channels of config 3's input in one launch (gsdrxFmDemodMulti)",
+            "us_per_launch": round(t * 1e6, 2), "us_per_channel": round(t * 1e6 / C, 2),
+            "channel_msamples_per_s": round(C * n_in / t / 1e6, 1),
+            "speedup_vs_single_calls": round(C * out["fm_chain"]["us_per_launch"] / (t * 1e6), 2)}
+        del ym
     del xs
     # int8 I/Q front end fused into the filter: 2 instead of 8 input bytes per sample
     x8s = [torch.randint(-128, 128, (2 * n_in,), dtype=torch.int8, device=device, generator=g) for _ in range(ROTATE)]

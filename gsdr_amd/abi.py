@@ -78,6 +78,8 @@ SIGNATURES = {
     "gsdrxFirFCInt8": (_err, [_sz, _p, _sz, _p, _p, _sz, _i32, _p]),
     "gsdrxFirFCInt8Variant": (_err, [_int, _sz, _p, _sz, _p, _p, _sz, _i32, _p]),
     "gsdrxFmDemodInt8": (_err, [_f, _f, _f, _f, _u32, _sz, _p, _sz, _p, _p, _sz, _i32, _p]),
+    "gsdrxFmDemodMulti": (_err, [_f, _f, _p, _p, _u32, _u32, _sz, _p, _sz, _int, _p, _p, _sz, _i32, _p]),
+    "gsdrxAmDemodMulti": (_err, [_f, _f, _p, _u32, _u32, _sz, _p, _sz, _int, _p, _p, _sz, _i32, _p]),
     # stream.h
     "gsdrxStreamCreate": (_err, [ctypes.POINTER(_p), _int, _int, _u32, _p, _sz, _f, _f, _f, _f, _sz, _i32]),
     "gsdrxStreamOutputsFor": (_sz, [_p, _sz]),

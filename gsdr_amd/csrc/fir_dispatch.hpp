@@ -310,6 +310,53 @@ hipError_t launch_d4_complex(const FirJob& j, hipStream_t s) {
   }
 }
 
+// Multi-channel chain (k_fir_multi): one launch per group of <= kMaxMultiChannels channels. Returns
+// hipErrorNotSupported when the shape does not apply (the caller then runs the channels one by one).
+template <class TapT, class InT, int D, int R, int JC, int WG, int MODE>
+hipError_t launch_multi(const FirJob& j, const MultiParams& mp, hipStream_t s) {
+  using Geo = TileGeo<InT, D, R, WG>;
+  constexpr int HMAX = 1;
+  constexpr int BPT = Geo::SG * (Geo::KT / Geo::ROUT) / WG;
+  FirParams p = make_params(j);
+  const uint64_t rows = ceil_div<uint64_t>(j.T, (uint64_t)D);
+  const uint64_t nch = ceil_div<uint64_t>(rows, (uint64_t)JC);
+  const uint64_t span = nch * JC * D;
+  if (span > 0x40000000ull) return hipErrorNotSupported;
+  const uint64_t NG = ((uint64_t)(Geo::KT - 1) * D + span + Geo::G - 1) / Geo::G;
+  if (NG > (uint64_t)(BPT + HMAX) * WG) return hipErrorNotSupported;  // halo does not fit the registers
+  const size_t lds = poly_lds_bytes<InT, D, R, WG>((uint32_t)span, MODE);
+  if (lds > kMaxTileLds) return hipErrorNotSupported;
+  p.nch = (uint32_t)nch;
+  const uint32_t stride = (MODE == kModeFm) ? Geo::KT - 1 : Geo::KT;
+  p.tile_stride = stride;
+  const uint64_t tiles = ceil_div<uint64_t>(j.N, stride);
+  if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
+  constexpr uint64_t A = SampleT<InT>::kSrcAlign;
+  const bool vec = (reinterpret_cast<uintptr_t>(j.in) % A) == 0 && ((uint64_t)stride * D * sizeof(InT)) % A == 0;
+  if (vec) {
+    k_fir_multi<TapT, InT, D, R, JC, WG, HMAX, true, MODE, true><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p, mp);
+  } else {
+    k_fir_multi<TapT, InT, D, R, JC, WG, HMAX, false, MODE, true><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p, mp);
+  }
+  return launch_status();
+}
+
+// same D and JC as launch_fir's single-channel kernels -> identical per-output MAC order
+template <class InT, int MODE>
+hipError_t launch_multi_chain(const FirJob& j, const MultiParams& mp, hipStream_t s) {
+  if (j.T > (1u << 26)) return hipErrorNotSupported;
+  switch (j.D) {
+    case 2:
+      return launch_multi<float, InT, 2, 8, 16, 128, MODE>(j, mp, s);
+    case 4:
+      return launch_multi<float, InT, 4, 4, 16, 256, MODE>(j, mp, s);
+    case 8:
+      return launch_multi<float, InT, 8, 2, 8, 256, MODE>(j, mp, s);
+    default:
+      return hipErrorNotSupported;
+  }
+}
+
 // tile-shape sweep for the int8 front end (gsdrxFirFCInt8Variant): the shapes of launch_d4_complex
 // whose staging is generic over the input type
 inline hipError_t launch_d4_int8(const FirJob& j, hipStream_t s) {
@@ -341,6 +388,21 @@ inline hipError_t launch_d4_int8(const FirJob& j, hipStream_t s) {
   }
 }
 
+// A default shape whose tile does not fit kMaxTileLds at the headline tap count would silently run
+// the generic kernel: reject that at compile time (FM layout = the largest).
+template <class InT, int D, int R, int JC, int WG>
+constexpr bool fits_lds_at_t127() {
+  constexpr uint32_t rows = (127 + D - 1) / D;
+  constexpr uint32_t span = (rows + JC - 1) / JC * JC * D;
+  return poly_lds_bytes<InT, D, R, WG>(span, kModeFm) <= kMaxTileLds;
+}
+
+template <class TapT, class InT, int D, int R, int JC, int WG, int MODE>
+hipError_t launch_poly_default(const FirJob& j, hipStream_t s) {
+  static_assert(fits_lds_at_t127<InT, D, R, JC, WG>(), "default polyphase shape exceeds the LDS budget");
+  return launch_poly<TapT, InT, D, R, JC, WG, MODE, 0, true>(j, s);
+}
+
 template <class TapT, class InT, int MODE>
 hipError_t launch_fir(const FirJob& j, hipStream_t s) {
   constexpr bool kComplexIn = SampleT<InT>::kPerGranule == 2;
@@ -353,11 +415,11 @@ hipError_t launch_fir(const FirJob& j, hipStream_t s) {
     }
     switch (j.D) {
       case 2:
-        return launch_poly<TapT, InT, 2, 8, 16, 128, MODE, 0, true>(j, s);
+        return launch_poly_default<TapT, InT, 2, 8, 16, 128, MODE>(j, s);
       case 4:
-        return launch_poly<TapT, InT, 4, 4, 16, 256, MODE, 0, true>(j, s);
+        return launch_poly_default<TapT, InT, 4, 4, 16, 256, MODE>(j, s);
       case 8:
-        return launch_poly<TapT, InT, 8, 8, 8, 128, MODE, 0, true>(j, s);
+        return launch_poly_default<TapT, InT, 8, 2, 8, 256, MODE>(j, s);
       default:
         return launch_generic<TapT, InT, MODE>(j, s);
     }
@@ -366,15 +428,15 @@ hipError_t launch_fir(const FirJob& j, hipStream_t s) {
       case 1:
         return launch_contig<TapT, InT, 1, 8, 16, 256, MODE>(j, s);
       case 2:
-        return launch_poly<TapT, InT, 2, 8, 16, 128, MODE, 0, true>(j, s);
+        return launch_poly_default<TapT, InT, 2, 8, 16, 128, MODE>(j, s);
       case 4:
         if constexpr (MODE == kModeFir && std::is_same<TapT, float>::value) {
           if (j.variant >= 0) return launch_d4_complex<TapT, InT, MODE>(j, s);
         }
         // 4 waves/SIMD (16 per CU): the shape that measured fastest at T = 127
-        return launch_poly<TapT, InT, 4, 4, 16, 256, MODE, 0, true>(j, s);
+        return launch_poly_default<TapT, InT, 4, 4, 16, 256, MODE>(j, s);
       case 8:
-        return launch_poly<TapT, InT, 8, 8, 8, 128, MODE, 0, true>(j, s);
+        return launch_poly_default<TapT, InT, 8, 2, 8, 256, MODE>(j, s);
       default:
         return launch_generic<TapT, InT, MODE>(j, s);
     }
@@ -385,9 +447,9 @@ hipError_t launch_fir(const FirJob& j, hipStream_t s) {
       case 2:
         return launch_contig<TapT, InT, 2, 8, 16, 256, MODE>(j, s);
       case 4:
-        return launch_poly<TapT, InT, 4, 8, 8, 128, MODE, 0, true>(j, s);
+        return launch_poly_default<TapT, InT, 4, 8, 8, 128, MODE>(j, s);
       case 8:
-        return launch_poly<TapT, InT, 8, 8, 8, 128, MODE, 0, true>(j, s);
+        return launch_poly_default<TapT, InT, 8, 8, 8, 128, MODE>(j, s);
       default:
         return launch_generic<TapT, InT, MODE>(j, s);
     }

@@ -550,6 +550,88 @@ __global__ __launch_bounds__(WG) void k_fir_poly(FirParams p) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// Kernel 1m: multi-channel NCO + FIR + demodulator (the intent of the
+// reference's dead k_Fm4x, src/fm.cu:71-179). The workgroup loads its input tile from HBM into
+// registers ONCE, then for each channel mixes it with that channel's NCO into the LDS tile, runs the
+// polyphase core and writes the channel's demodulated outputs. HBM input traffic is paid once for
+// all channels; the per-output arithmetic (NCO phasor, MAC order, epilogue) is the single-channel
+// kernel's, so channel c is bit-identical to gsdrFmDemod / gsdrAmDemod with its own frequency.
+// ------------------------------------------------------------------------------------------------
+constexpr int kMaxMultiChannels = 16;
+
+struct MultiParams {
+  uint32_t count;                     // channels in this launch
+  uint32_t inc[kMaxMultiChannels];    // NCO phase increment per channel
+  float gain[kMaxMultiChannels];      // FM gain per channel
+};
+
+template <class TapT, class InT, int D, int R, int JC, int WG, int HMAX, bool VEC, int MODE, bool NT>
+__global__ __launch_bounds__(WG) void k_fir_multi(FirParams p, MultiParams mp) {
+  using Geo = TileGeo<InT, D, R, WG>;
+  using OutT = typename Product<TapT, InT>::type;
+  constexpr int G = Geo::G;
+  constexpr int BPT = Geo::SG * (Geo::KT / Geo::ROUT) / WG;
+  static_assert(MODE != kModeFir, "channels differ by their NCO");
+
+  extern __shared__ __attribute__((aligned(16))) float4 lds[];
+  const InT* __restrict__ in = reinterpret_cast<const InT*>(p.in);
+  const uint64_t out0 = (uint64_t)blockIdx.x * p.tile_stride;
+  const uint64_t S0 = out0 * D;
+  const uint32_t span = p.nch * JC * D;
+  const uint32_t NG = ((Geo::KT - 1) * D + span + G - 1) / G;
+  const uint32_t tid = threadIdx.x;
+
+  // the raw tile, held in registers across the channel loop (loaded as stage_tile does)
+  float4 body[BPT];
+  float4 halo[HMAX];
+  const bool whole = VEC && (S0 + (uint64_t)NG * G <= p.L);
+  if (whole) {
+    if constexpr (std::is_same<InT, Iq8>::value) {
+      const uint32_t* __restrict__ src = reinterpret_cast<const uint32_t*>(in + S0);
+#pragma unroll
+      for (int k = 0; k < BPT; ++k) body[k] = iq8x2_granule(NT ? __builtin_nontemporal_load(src + k * WG + tid) : src[k * WG + tid]);
+    } else {
+      const float4* __restrict__ src = reinterpret_cast<const float4*>(in + S0);
+#pragma unroll
+      for (int k = 0; k < BPT; ++k) body[k] = NT ? load16_nt(src + k * WG + tid) : src[k * WG + tid];
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < BPT; ++k) body[k] = load_granule<InT, VEC>(in, S0 + (uint64_t)(k * WG + tid) * G, p.L);
+  }
+#pragma unroll
+  for (int k = 0; k < HMAX; ++k) {
+    const uint32_t g = BPT * WG + k * WG + tid;
+    halo[k] = g < NG ? load_granule<InT, VEC>(in, S0 + (uint64_t)g * G, p.L) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+
+  float2* xs = reinterpret_cast<float2*>(lds + Geo::padded(NG - 1) + 1);
+  for (uint32_t c = 0; c < mp.count; ++c) {
+    FirParams pc = p;
+    pc.nco_inc = mp.inc[c];
+    pc.fm_gain = mp.gain[c];
+    pc.out = reinterpret_cast<float*>(p.out) + (uint64_t)c * p.N;
+#pragma unroll
+    for (int k = 0; k < BPT; ++k) {
+      const uint32_t g = k * WG + tid;
+      lds[Geo::padded(g)] = stage_transform<InT, MODE>(body[k], (uint32_t)S0 + g * G, pc);
+    }
+#pragma unroll
+    for (int k = 0; k < HMAX; ++k) {
+      const uint32_t g = BPT * WG + k * WG + tid;
+      if (g < NG) lds[Geo::padded(g)] = stage_transform<InT, MODE>(halo[k], (uint32_t)S0 + g * G, pc);
+    }
+    __syncthreads();
+    OutT acc[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) set_zero(acc[r]);
+    poly_compute<TapT, InT, D, R, JC, WG>(lds, pc, acc);
+    tile_epilogue<MODE, OutT, R, WG>(pc, out0, acc, xs);
+    __syncthreads();  // the next channel overwrites the tile
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Kernel 1c: column-split polyphase kernel (D = 2G: two granule columns per row, e.g. complex D = 4).
 // Waves come in pairs over the same outputs: the even wave of a pair accumulates column 0 (phases
 // 0..G-1), the odd wave column 1. The column is wave-uniform, so a wave needs only NCH*JC*G taps --
@@ -937,7 +1019,7 @@ __global__ __launch_bounds__(256) void k_fir_generic(FirParams p) {
 // Host-side sizing helpers
 // ------------------------------------------------------------------------------------------------
 template <class InT, int D, int R, int WG>
-inline size_t poly_lds_bytes(uint32_t span_samples, int mode, size_t tap_bytes = 0) {
+constexpr size_t poly_lds_bytes(uint32_t span_samples, int mode, size_t tap_bytes = 0) {
   using Geo = TileGeo<InT, D, R, WG>;
   const uint32_t NG = ((Geo::KT - 1) * D + span_samples + Geo::G - 1) / Geo::G;
   size_t bytes = (size_t)(Geo::padded(NG - 1) + 1) * 16u;

@@ -64,6 +64,56 @@ static hipError_t chain_entry(int mode, float fs, float tune, float chan, float 
                          : launch_fir<float, InT, kModeAm>(job, stream);
 }
 
+template <class InT>
+static hipError_t chain_multi_entry(int mode, float fs, float tune, const float* chans, const float* devs,
+                                    uint32_t count, uint32_t decimation, size_t firstSampleIndex, const float* taps,
+                                    size_t tapCount, const InT* input, float* output, size_t numOutputs,
+                                    int32_t device, hipStream_t stream) {
+  if (numOutputs == 0 || count == 0) return hipSuccess;
+  if (chans == nullptr || (mode == kModeFm && devs == nullptr)) return hipErrorInvalidValue;
+  if (decimation == 0 || output == nullptr || input == nullptr) return hipErrorInvalidValue;
+  if (tapCount > 0 && taps == nullptr) return hipErrorInvalidValue;
+  for (uint32_t c0 = 0; c0 < count; c0 += kMaxMultiChannels) {
+    const uint32_t n = count - c0 < (uint32_t)kMaxMultiChannels ? count - c0 : (uint32_t)kMaxMultiChannels;
+    MultiParams mp{};
+    mp.count = n;
+    for (uint32_t c = 0; c < n; ++c) {
+      if (!nco_increment(fs, tune, chans[c0 + c], &mp.inc[c])) return hipErrorInvalidValue;
+      mp.gain[c] = mode == kModeFm ? fs / (2.0f * kPiF * devs[c0 + c]) : 0.0f;
+    }
+    float* out = output + (size_t)c0 * numOutputs;
+    hipError_t e = hipErrorNotSupported;
+    if (tapCount > 0) {
+      FirJob job;
+      job.in = input;
+      job.taps = taps;
+      job.out = out;
+      job.D = decimation;
+      job.T = tapCount;
+      job.N = numOutputs;
+      job.mode = mode;
+      job.nco_n0 = (uint32_t)firstSampleIndex;
+      job.L = mode == kModeFm ? numOutputs * (size_t)decimation + tapCount
+                              : (numOutputs - 1) * (size_t)decimation + tapCount;
+      DeviceScope scope(device);
+      if (scope.status() != hipSuccess) return scope.status();
+      e = mode == kModeFm ? launch_multi_chain<InT, kModeFm>(job, mp, stream)
+                          : launch_multi_chain<InT, kModeAm>(job, mp, stream);
+    }
+    if (e == hipErrorNotSupported) {  // one channel at a time through the single-channel path
+      (void)hipGetLastError();
+      e = hipSuccess;
+      for (uint32_t c = 0; c < n && e == hipSuccess; ++c) {
+        e = chain_entry(mode, fs, tune, chans[c0 + c], mode == kModeFm ? devs[c0 + c] : 1.0f, decimation,
+                        firstSampleIndex, taps, tapCount, input, out + (size_t)c * numOutputs, numOutputs, device,
+                        stream);
+      }
+    }
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
 }  // namespace gsdr
 
 GSDR_C_LINKAGE hipError_t gsdrFmDemod(float rfSampleRate, float tuningFrequency, float channelFrequency,
@@ -113,3 +163,38 @@ GSDR_C_LINKAGE uint32_t gsdrNcoPhaseIncrement(float rfSampleRate, float tuningFr
 }
 
 GSDR_C_LINKAGE const char* gsdrVersion(void) GSDR_NO_EXCEPT { return "gsdr-mi355x 0.1.0 (gfx950)"; }
+
+GSDR_C_LINKAGE hipError_t gsdrxFmDemodMulti(float rfSampleRate, float tuningFrequency, const float* channelFrequencies,
+                                            const float* frequencyDeviations, uint32_t numChannels,
+                                            uint32_t decimation, size_t firstSampleIndex, const float* lowPassTaps,
+                                            size_t numLowPassTaps, int sampleFormat, const void* input, float* output,
+                                            size_t numOutputs, int32_t cudaDevice,
+                                            hipStream_t cudaStream) GSDR_NO_EXCEPT {
+  if (sampleFormat == GSDRX_SAMPLES_CS8) {
+    return gsdr::chain_multi_entry(gsdr::kModeFm, rfSampleRate, tuningFrequency, channelFrequencies,
+                                   frequencyDeviations, numChannels, decimation, firstSampleIndex, lowPassTaps,
+                                   numLowPassTaps, static_cast<const gsdr::Iq8*>(input), output, numOutputs,
+                                   cudaDevice, cudaStream);
+  }
+  if (sampleFormat != GSDRX_SAMPLES_CF32) return hipErrorInvalidValue;
+  return gsdr::chain_multi_entry(gsdr::kModeFm, rfSampleRate, tuningFrequency, channelFrequencies,
+                                 frequencyDeviations, numChannels, decimation, firstSampleIndex, lowPassTaps,
+                                 numLowPassTaps, static_cast<const float2*>(input), output, numOutputs, cudaDevice,
+                                 cudaStream);
+}
+
+GSDR_C_LINKAGE hipError_t gsdrxAmDemodMulti(float rfSampleRate, float tuningFrequency, const float* channelFrequencies,
+                                            uint32_t numChannels, uint32_t decimation, size_t firstSampleIndex,
+                                            const float* lowPassTaps, size_t numLowPassTaps, int sampleFormat,
+                                            const void* input, float* output, size_t numElements, int32_t cudaDevice,
+                                            hipStream_t cudaStream) GSDR_NO_EXCEPT {
+  if (sampleFormat == GSDRX_SAMPLES_CS8) {
+    return gsdr::chain_multi_entry(gsdr::kModeAm, rfSampleRate, tuningFrequency, channelFrequencies, nullptr,
+                                   numChannels, decimation, firstSampleIndex, lowPassTaps, numLowPassTaps,
+                                   static_cast<const gsdr::Iq8*>(input), output, numElements, cudaDevice, cudaStream);
+  }
+  if (sampleFormat != GSDRX_SAMPLES_CF32) return hipErrorInvalidValue;
+  return gsdr::chain_multi_entry(gsdr::kModeAm, rfSampleRate, tuningFrequency, channelFrequencies, nullptr,
+                                 numChannels, decimation, firstSampleIndex, lowPassTaps, numLowPassTaps,
+                                 static_cast<const float2*>(input), output, numElements, cudaDevice, cudaStream);
+}

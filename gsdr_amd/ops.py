@@ -17,7 +17,7 @@ __all__ = [
     "qpsk_modulate_templated", "qpsk_demodulate_templated",
     "qpsk256_init", "qpsk256_modulate", "qpsk256_demodulate", "qpsk256_modulate_4x", "qpsk256_demodulate_4x",
     "nco_phase_increment", "stream_of",
-    "add_const", "multiply", "add_to_magnitude", "abs_", "cosine", "int8_to_norm_float",
+    "fm_demod_multi", "am_demod_multi", "add_const", "multiply", "add_to_magnitude", "abs_", "cosine", "int8_to_norm_float",
 ]
 
 
@@ -148,6 +148,45 @@ def am_demod(x, taps, rf_sample_rate, tuning_frequency, channel_frequency, decim
                                          first_sample_index, _ptr(taps), T, _ptr(x), _ptr(out), num_outputs,
                                          _dev(x), stream_of(x)))
     return out
+
+
+def _multi(name, x, taps, fs, tune, chans, devs, decimation, first_sample_index, num_outputs, fm):
+    import ctypes
+
+    if x.dtype not in (torch.complex64, torch.int8):
+        raise TypeError(f"input: expected complex64 or int8 I/Q, got {x.dtype}")
+    _require(x, x.dtype, "input")
+    _require(taps, torch.float32, "taps")
+    T, L = taps.numel(), _nsamp(x)
+    if num_outputs is None:
+        num_outputs = max(0, (L - T) // decimation) if fm else ((L - T) // decimation + 1 if L >= T else 0)
+    need = num_outputs * decimation + T if fm else (num_outputs - 1) * decimation + T
+    if num_outputs > 0:
+        _require_samples(x, x.dtype, "input", need)
+    C = len(chans)
+    out = torch.empty((C, num_outputs), dtype=torch.float32, device=x.device)
+    fa = (ctypes.c_float * max(C, 1))(*chans)
+    args = [fs, tune, fa]
+    if fm:
+        args.append((ctypes.c_float * max(C, 1))(*devs))
+    args += [C, decimation, first_sample_index, _ptr(taps), T, 1 if x.dtype == torch.int8 else 0, _ptr(x), _ptr(out),
+             num_outputs, _dev(x), stream_of(x)]
+    check(name, getattr(lib, name)(*args))
+    return out
+
+
+def fm_demod_multi(x, taps, rf_sample_rate, tuning_frequency, channel_frequencies, frequency_deviations,
+                   decimation, first_sample_index=0, num_outputs=None):
+    """gsdrxFmDemodMulti: out[c] = gsdrFmDemod with channel_frequencies[c], frequency_deviations[c]."""
+    return _multi("gsdrxFmDemodMulti", x, taps, rf_sample_rate, tuning_frequency, channel_frequencies,
+                  frequency_deviations, decimation, first_sample_index, num_outputs, True)
+
+
+def am_demod_multi(x, taps, rf_sample_rate, tuning_frequency, channel_frequencies, decimation,
+                   first_sample_index=0, num_outputs=None):
+    """gsdrxAmDemodMulti: out[c] = gsdrAmDemod with channel_frequencies[c]."""
+    return _multi("gsdrxAmDemodMulti", x, taps, rf_sample_rate, tuning_frequency, channel_frequencies, None,
+                  decimation, first_sample_index, num_outputs, False)
 
 
 def quad_fm_demod(x, gain, num_outputs=None, out=None):

@@ -13,6 +13,10 @@
 #include <stddef.h>
 #include <stdint.h>
 
+/* input sample formats taken by the multi-channel chains and the streaming object (stream.h) */
+#define GSDRX_SAMPLES_CF32 0 /* hipFloatComplex */
+#define GSDRX_SAMPLES_CS8 1  /* interleaved int8 I/Q, converted as gsdrInt8ToNormFloat */
+
 /** Library version string, e.g. "gsdr-mi355x 0.1.0 (gfx950)". */
 GSDR_C_LINKAGE GSDR_PUBLIC const char* gsdrVersion(void) GSDR_NO_EXCEPT;
 
@@ -100,6 +104,48 @@ GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxAmDemodInt8(
     const float* lowPassTaps,
     size_t numLowPassTaps,
     const int8_t* input,
+    float* output,
+    size_t numElements,
+    int32_t cudaDevice,
+    hipStream_t cudaStream) GSDR_NO_EXCEPT;
+
+/*
+ * Multi-channel chains (the intent of the reference's unused k_Fm4x,
+ * src/fm.cu:71-179): numChannels channels of one RF input, each with its own channel frequency (and
+ * FM deviation), sharing the tuning frequency, decimation, taps and firstSampleIndex. Channel c writes
+ * output[c * numOutputs + m]; its outputs are bit-identical to gsdrFmDemod / gsdrAmDemod (or the
+ * Int8 variants) called with channelFrequencies[c] (and frequencyDeviations[c]). For decimation 2, 4
+ * and 8 one kernel reads each input tile from HBM once for up to 16 channels; other decimations run
+ * the channels one after another. channelFrequencies / frequencyDeviations are host arrays.
+ */
+GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxFmDemodMulti(
+    float rfSampleRate,
+    float tuningFrequency,
+    const float* channelFrequencies,
+    const float* frequencyDeviations,
+    uint32_t numChannels,
+    uint32_t decimation,
+    size_t firstSampleIndex,
+    const float* lowPassTaps,
+    size_t numLowPassTaps,
+    int sampleFormat,
+    const void* input,
+    float* output,
+    size_t numOutputs,
+    int32_t cudaDevice,
+    hipStream_t cudaStream) GSDR_NO_EXCEPT;
+
+GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxAmDemodMulti(
+    float rfSampleRate,
+    float tuningFrequency,
+    const float* channelFrequencies,
+    uint32_t numChannels,
+    uint32_t decimation,
+    size_t firstSampleIndex,
+    const float* lowPassTaps,
+    size_t numLowPassTaps,
+    int sampleFormat,
+    const void* input,
     float* output,
     size_t numElements,
     int32_t cudaDevice,

@@ -28,6 +28,7 @@
 #define GSDR_STREAM_H_
 
 #include <gsdr/gsdr_export.h>
+#include <gsdr/gsdr_ext.h>
 #include <gsdr/util.h>
 #include <hip/hip_runtime_api.h>
 #include <stddef.h>
@@ -36,9 +37,6 @@
 #define GSDRX_STREAM_FIR 0
 #define GSDRX_STREAM_FM 1
 #define GSDRX_STREAM_AM 2
-
-#define GSDRX_SAMPLES_CF32 0
-#define GSDRX_SAMPLES_CS8 1
 
 typedef struct gsdrxStream_t* gsdrxStream;
 

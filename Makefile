@@ -19,11 +19,6 @@ $(BUILD)/%.o: gsdr_amd/csrc/%.hip $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-# tuning probes: scalar-FMA build of the headline kernel (see fir_probe.hip)
-$(BUILD)/fir_probe.o: gsdr_amd/csrc/fir_probe.hip $(HDRS)
-	@mkdir -p $(BUILD)
-	$(HIPCC) $(HIPFLAGS) -fno-slp-vectorize -c $< -o $@
-
 gsdr_amd/libgsdr.so: $(OBJS)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -Wl,-rpath,/opt/rocm/lib $(OBJS) -o $@
 

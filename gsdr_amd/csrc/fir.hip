@@ -75,24 +75,16 @@ hipError_t launch_stream_probe(const FirJob& j, hipStream_t s, bool nt) {
   return launch_status();
 }
 
-// Packed-FMA tuning probes (gsdrxFirFCVariant 103+): 103 compute-only at the default shape,
-// 104 compute-only / 105 staging-only at the WG=256, R=4 shape.
-hipError_t launch_fc_probe_packed(const FirJob& j, hipStream_t s) {
+// Ablation probes (gsdrxFirFCVariant >= 100) used for the energy split in DESIGN.md section 3.1:
+// the default shape with only one half of its work.
+hipError_t launch_fc_probe(const FirJob& j, hipStream_t s) {
   switch (j.variant) {
-    case 103:
-      return launch_poly<float, float2, 4, 8, 16, 128, kModeFir, 2>(j, s);
-    case 104:
-      return launch_poly<float, float2, 4, 4, 16, 256, kModeFir, 2>(j, s);
-    case 105:
+    case 104:  // compute only (no staging; the tile holds whatever LDS held)
+      return launch_poly<float, float2, 4, 4, 16, 256, kModeFir, 2, true>(j, s);
+    case 105:  // staging only, plain loads
       return launch_poly<float, float2, 4, 4, 16, 256, kModeFir, 1>(j, s);
-    case 106:  // WG=256, R=4 with non-temporal input loads
-      return launch_poly<float, float2, 4, 4, 16, 256, kModeFir, 0, true>(j, s);
-    case 107:  // staging only, non-temporal
+    case 107:  // staging only, non-temporal loads
       return launch_poly<float, float2, 4, 4, 16, 256, kModeFir, 1, true>(j, s);
-    case 108:  // WG=512, R=2 (more waves, smaller windows)
-      return launch_poly<float, float2, 4, 2, 16, 512, kModeFir>(j, s);
-    case 109:  // WG=128, R=4
-      return launch_poly<float, float2, 4, 4, 16, 128, kModeFir>(j, s);
     case 110:
     case 111:
       return launch_stream_probe(j, s, j.variant == 111);

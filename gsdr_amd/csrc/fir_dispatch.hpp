@@ -61,8 +61,7 @@ hipError_t launch_generic(const FirJob& j, hipStream_t s) {
   return launch_status();
 }
 
-template <class TapT, class InT, int D, int R, int JC, int WG, int MODE, int ABL = 0, bool NT = false,
-          bool TL = false>
+template <class TapT, class InT, int D, int R, int JC, int WG, int MODE, int ABL = 0, bool NT = false>
 hipError_t launch_poly(const FirJob& j, hipStream_t s) {
   using Geo = TileGeo<InT, D, R, WG>;
   FirParams p = make_params(j);
@@ -70,7 +69,7 @@ hipError_t launch_poly(const FirJob& j, hipStream_t s) {
   const uint64_t nch = ceil_div<uint64_t>(rows, (uint64_t)JC);
   const uint64_t span = nch * JC * D;
   if (span > 0x40000000ull) return launch_generic<TapT, InT, MODE>(j, s);
-  const size_t lds = poly_lds_bytes<InT, D, R, WG>((uint32_t)span, MODE, TL ? span * sizeof(TapT) : 0);
+  const size_t lds = poly_lds_bytes<InT, D, R, WG>((uint32_t)span, MODE);
   if (lds > kMaxTileLds) return launch_generic<TapT, InT, MODE>(j, s);
   p.nch = (uint32_t)nch;
   const uint32_t stride = (MODE == kModeFm) ? Geo::KT - 1 : Geo::KT;
@@ -80,9 +79,9 @@ hipError_t launch_poly(const FirJob& j, hipStream_t s) {
   constexpr uint64_t A = SampleT<InT>::kSrcAlign;
   const bool vec = (reinterpret_cast<uintptr_t>(j.in) % A) == 0 && ((uint64_t)stride * D * sizeof(InT)) % A == 0;
   if (vec) {
-    k_fir_poly<TapT, InT, D, R, JC, WG, true, MODE, ABL, NT, TL><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
+    k_fir_poly<TapT, InT, D, R, JC, WG, true, MODE, ABL, NT><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
   } else {
-    k_fir_poly<TapT, InT, D, R, JC, WG, false, MODE, ABL, NT, TL><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
+    k_fir_poly<TapT, InT, D, R, JC, WG, false, MODE, ABL, NT><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
   }
   return launch_status();
 }
@@ -110,203 +109,38 @@ hipError_t launch_contig(const FirJob& j, hipStream_t s) {
   return launch_status();
 }
 
-// Workgroups per CU that the hardware keeps resident for `kernel` at `lds` bytes (occupancy query,
-// capped by the LDS budget), times the CU count: the persistent grid.
-inline uint32_t persistent_grid(const void* kernel, int wg, size_t lds, int oversubscribe) {
-  int dev = 0, cus = 0, per_cu = 0, lds_cu = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return 0;
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-  if (hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess) {
-    lds_cu = 160 * 1024;
-  }
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, wg, lds) != hipSuccess) return 0;
-  const int by_lds = lds > 0 ? (int)((size_t)lds_cu / lds) : per_cu;
-  if (by_lds < per_cu) per_cu = by_lds;
-  if (per_cu < 1) per_cu = 1;
-  const uint32_t grid = (uint32_t)(cus * per_cu * (oversubscribe < 1 ? 1 : oversubscribe));
-  static bool debug = getenv("GSDR_DEBUG") != nullptr;
-  if (debug) {
-    fprintf(stderr, "gsdr: persistent grid %u = %d CUs x %d WG/CU x %d (wg %d, lds %zu B, lds/CU %d)\n", grid, cus,
-            per_cu, oversubscribe, wg, lds, lds_cu);
-  }
-  return grid;
-}
-
-// Persistent, register-prefetching polyphase kernel (k_fir_poly_pipe). Falls back to the one-tile
-// kernel when the halo does not fit the HALO registers per thread.
-template <class TapT, class InT, int D, int R, int JC, int WG, int HALO, int MODE>
-hipError_t launch_poly_pipe(const FirJob& j, hipStream_t s, int oversubscribe = 1) {
-  using Geo = TileGeo<InT, D, R, WG>;
-  FirParams p = make_params(j);
-  const uint64_t rows = ceil_div<uint64_t>(j.T, (uint64_t)D);
-  const uint64_t nch = ceil_div<uint64_t>(rows, (uint64_t)JC);
-  const uint64_t span = nch * JC * D;
-  const uint64_t NG = ((uint64_t)(Geo::KT - 1) * D + span + Geo::G - 1) / Geo::G;
-  if (NG > (uint64_t)(Geo::SG + HALO) * WG) return launch_poly<TapT, InT, D, R, JC, WG, MODE>(j, s);
-  const size_t lds = poly_lds_bytes<InT, D, R, WG>((uint32_t)span, MODE);
-  if (lds > kMaxTileLds) return launch_generic<TapT, InT, MODE>(j, s);
-  p.nch = (uint32_t)nch;
-  const uint32_t stride = (MODE == kModeFm) ? Geo::KT - 1 : Geo::KT;
-  p.tile_stride = stride;
-  const uint64_t tiles = ceil_div<uint64_t>(j.N, stride);
-  if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
-  const bool vec = aligned16(j.in) && ((uint64_t)stride * D * sizeof(InT)) % 16 == 0;
-  if (!vec) return launch_poly<TapT, InT, D, R, JC, WG, MODE>(j, s);
-  const void* kern = reinterpret_cast<const void*>(&k_fir_poly_pipe<TapT, InT, D, R, JC, WG, HALO, MODE>);
-  uint32_t grid = persistent_grid(kern, WG, lds, oversubscribe);
-  if (grid == 0) return hipErrorInvalidDevice;
-  if (grid > tiles) grid = (uint32_t)tiles;
-  k_fir_poly_pipe<TapT, InT, D, R, JC, WG, HALO, MODE><<<dim3(grid), dim3(WG), lds, s>>>(p, (uint32_t)tiles);
-  return launch_status();
-}
-
-// Persistent LDS-DMA pipeline (k_fir_poly_dma), FIR mode, 16-byte aligned input only; otherwise the
-// one-tile kernel.
-template <class TapT, class InT, int D, int R, int JC, int WG, bool TL = false>
-hipError_t launch_poly_dma(const FirJob& j, hipStream_t s) {
-  using Geo = TileGeo<InT, D, R, WG>;
-  FirParams p = make_params(j);
-  const uint64_t rows = ceil_div<uint64_t>(j.T, (uint64_t)D);
-  const uint64_t nch = ceil_div<uint64_t>(rows, (uint64_t)JC);
-  const uint64_t span = nch * JC * D;
-  const uint64_t stride = Geo::KT;
-  const bool vec = aligned16(j.in) && (stride * D * sizeof(InT)) % 16 == 0;
-  if (!vec || span > (1u << 20)) return launch_poly<TapT, InT, D, R, JC, WG, kModeFir>(j, s);
-  const uint64_t NG = ((uint64_t)(Geo::KT - 1) * D + span + Geo::G - 1) / Geo::G;
-  const uint64_t NGP = Geo::padded((uint32_t)(NG - 1)) + 1;
-  const uint32_t slots = (uint32_t)ceil_div<uint64_t>(NGP, WG) * WG;
-  const size_t lds = 2ull * slots * 16u + (TL ? span * sizeof(TapT) : 0);
-  if (lds > 160 * 1024) return launch_poly<TapT, InT, D, R, JC, WG, kModeFir>(j, s);
-  p.nch = (uint32_t)nch;
-  p.tile_stride = (uint32_t)stride;
-  const uint64_t tiles = ceil_div<uint64_t>(j.N, stride);
-  if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
-  const void* kern = reinterpret_cast<const void*>(&k_fir_poly_dma<TapT, InT, D, R, JC, WG, TL>);
-  if (lds > 64 * 1024) {
-    const hipError_t st = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (st != hipSuccess) return st;
-  }
-  uint32_t grid = persistent_grid(kern, WG, lds, 1);
-  if (grid == 0) return hipErrorInvalidDevice;
-  if (grid > tiles) grid = (uint32_t)tiles;
-  k_fir_poly_dma<TapT, InT, D, R, JC, WG, TL><<<dim3(grid), dim3(WG), lds, s>>>(p, (uint32_t)tiles, slots);
-  return launch_status();
-}
-
-// Column-split polyphase kernel (k_fir_poly_cs): D = 2 granules per row, FIR mode, NCH compile-time
-// chunk count (taps held in SGPRs for the whole kernel).
-template <class TapT, class InT, int D, int R, int JC, int WG, int NCH, bool NT = false>
-hipError_t launch_poly_cs(const FirJob& j, hipStream_t s) {
-  using Geo = TileGeo<InT, D, R, WG / 2>;
-  using OutT = typename Product<TapT, InT>::type;
-  FirParams p = make_params(j);
-  const uint64_t rows = ceil_div<uint64_t>(j.T, (uint64_t)D);
-  const uint64_t nch = ceil_div<uint64_t>(rows, (uint64_t)JC);
-  if (nch > (uint64_t)NCH) return launch_poly<TapT, InT, D, R, JC, WG, kModeFir>(j, s);
-  p.nch = NCH;  // fewer real chunks read zero taps (range-checked) -- same result
-  const uint32_t span = NCH * JC * D;
-  const uint32_t NG = ((Geo::KT - 1) * D + span + Geo::G - 1) / Geo::G;
-  const size_t lds = (size_t)(Geo::padded(NG - 1) + 1) * 16u + (size_t)(WG / 2) * R * sizeof(OutT);
-  if (lds > kMaxTileLds) return launch_generic<TapT, InT, kModeFir>(j, s);
-  p.tile_stride = Geo::KT;
-  const uint64_t tiles = ceil_div<uint64_t>(j.N, (uint64_t)Geo::KT);
-  if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
-  const bool vec = aligned16(j.in) && ((uint64_t)Geo::KT * D * sizeof(InT)) % 16 == 0;
-  if (vec) {
-    k_fir_poly_cs<TapT, InT, D, R, JC, WG, NCH, true, NT><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
-  } else {
-    k_fir_poly_cs<TapT, InT, D, R, JC, WG, NCH, false, NT><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
-  }
-  return launch_status();
-}
-
 // Tile-shape variants of the headline case (real taps, complex input, D = 4), selectable through
-// gsdrxFirFCVariant for tuning sweeps. Variant 0 is the default (WG = 256, R = 4, JC = 16);
-// variant 1 is the round-1 starting shape (WG = 128, R = 8).
-// Tuning probes (variant >= 100): 100-102 live in fir_probe.hip (compiled with -fno-slp-vectorize),
-// 103+ in fir.hip (packed-FMA build).
+// gsdrxFirFCVariant for tuning sweeps (all with non-temporal streaming unless noted):
+//   0 default WG=256 R=4 JC=16 | 1 WG=128 R=8 | 3 WG=64 R=8 | 4 WG=128 R=8 JC=32 | 5 WG=256 R=4 JC=8
+//   7 generic kernel | 8 default shape with plain (temporal) loads/stores | 24 WG=64 R=4 | 28 WG=128 R=4
+// Ablation probes (fir.hip): 104 compute only, 105 staging only, 107 staging only (non-temporal),
+// 110/111 streaming ceiling of this traffic mix (plain / non-temporal).
 hipError_t launch_fc_probe(const FirJob& j, hipStream_t s);
-hipError_t launch_fc_probe_packed(const FirJob& j, hipStream_t s);
 
 template <class TapT, class InT, int MODE>
 hipError_t launch_d4_complex(const FirJob& j, hipStream_t s) {
-  if (j.variant >= 103) return launch_fc_probe_packed(j, s);
   if (j.variant >= 100) return launch_fc_probe(j, s);
   switch (j.variant) {
+    case 0:
+      return launch_poly<TapT, InT, 4, 4, 16, 256, MODE, 0, true>(j, s);
     case 1:
-      return launch_poly<TapT, InT, 4, 8, 16, 128, MODE>(j, s);
-    case 2:
-      return launch_poly<TapT, InT, 4, 8, 16, 256, MODE>(j, s);
+      return launch_poly<TapT, InT, 4, 8, 16, 128, MODE, 0, true>(j, s);
     case 3:
-      return launch_poly<TapT, InT, 4, 8, 16, 64, MODE>(j, s);
+      return launch_poly<TapT, InT, 4, 8, 16, 64, MODE, 0, true>(j, s);
     case 4:
-      return launch_poly<TapT, InT, 4, 8, 32, 128, MODE>(j, s);
+      return launch_poly<TapT, InT, 4, 8, 32, 128, MODE, 0, true>(j, s);
     case 5:
-      return launch_poly<TapT, InT, 4, 4, 8, 256, MODE>(j, s);
-    case 6:
-      return launch_poly<TapT, InT, 4, 16, 16, 128, MODE>(j, s);
+      return launch_poly<TapT, InT, 4, 4, 8, 256, MODE, 0, true>(j, s);
     case 7:
       return launch_generic<TapT, InT, MODE>(j, s);
-    case 20:
-      return launch_poly_pipe<TapT, InT, 4, 4, 16, 256, 1, MODE>(j, s);
-    case 21:
-      return launch_poly_pipe<TapT, InT, 4, 4, 8, 256, 1, MODE>(j, s);
-    case 22:
-      return launch_poly_pipe<TapT, InT, 4, 4, 16, 128, 1, MODE>(j, s);
-    case 23:
-      return launch_poly_pipe<TapT, InT, 4, 4, 16, 256, 1, MODE>(j, s, 2);
-    case 24:  // single-wave workgroups: wave-local barriers, waves drift apart freely
-      return launch_poly<TapT, InT, 4, 4, 16, 64, MODE>(j, s);
-    case 25:
-      return launch_poly_pipe<TapT, InT, 4, 4, 16, 64, 1, MODE>(j, s);
-    case 26:
-      return launch_poly_pipe<TapT, InT, 4, 4, 8, 64, 1, MODE>(j, s);
-    case 27:
-      return launch_poly<TapT, InT, 4, 8, 16, 64, MODE>(j, s);
-    case 30:  // LDS-DMA double-buffered pipeline: 2 x 38 KB per WG -> 2 WGs (8 waves) per CU
-      return launch_poly_dma<TapT, InT, 4, 4, 16, 256>(j, s);
-    case 31:  // R = 2: 2 x 25 KB -> 3 WGs (12 waves) per CU
-      return launch_poly_dma<TapT, InT, 4, 2, 16, 256>(j, s);
-    case 32:  // WG = 512, R = 2: 8 waves in one WG per CU
-      return launch_poly_dma<TapT, InT, 4, 2, 16, 512>(j, s);
-    case 33:  // WG = 128, R = 4: 2 x 20 KB -> 3 WGs per CU
-      return launch_poly_dma<TapT, InT, 4, 4, 16, 128>(j, s);
-    case 40:  // default shape, taps staged in LDS
-      return launch_poly<TapT, InT, 4, 4, 16, 256, MODE, 0, false, true>(j, s);
-    case 41:  // R = 8, WG = 128, taps in LDS
-      return launch_poly<TapT, InT, 4, 8, 16, 128, MODE, 0, false, true>(j, s);
-    case 42:  // DMA pipeline, taps in LDS
-      return launch_poly_dma<TapT, InT, 4, 4, 16, 256, true>(j, s);
-    case 43:
-      return launch_poly_dma<TapT, InT, 4, 4, 16, 128, true>(j, s);
-    case 44:  // R = 4, WG = 256, JC = 32, taps in LDS
-      return launch_poly<TapT, InT, 4, 4, 32, 256, MODE, 0, false, true>(j, s);
-    case 45:
-      return launch_poly<TapT, InT, 4, 4, 8, 256, MODE, 0, false, true>(j, s);
-    case 46:
-      return launch_poly<TapT, InT, 4, 8, 8, 128, MODE, 0, false, true>(j, s);
-    case 47:
-      return launch_poly<TapT, InT, 4, 8, 8, 64, MODE, 0, false, true>(j, s);
-    case 50:  // column split, R = 8, 2 pairs of waves, taps in SGPRs once
-      return launch_poly_cs<TapT, InT, 4, 8, 16, 256, 2>(j, s);
-    case 51:
-      return launch_poly_cs<TapT, InT, 4, 4, 16, 256, 2>(j, s);
-    case 52:
-      return launch_poly_cs<TapT, InT, 4, 8, 16, 128, 2>(j, s);
-    case 53:
-      return launch_poly_cs<TapT, InT, 4, 4, 16, 512, 2>(j, s);
-    case 54:  // column split R = 8 with non-temporal loads and stores
-      return launch_poly_cs<TapT, InT, 4, 8, 16, 256, 2, true>(j, s);
-    case 55:  // default shape with non-temporal loads and stores
-      return launch_poly<TapT, InT, 4, 4, 16, 256, MODE, 0, true>(j, s);
-    case 56:
-      return launch_poly_cs<TapT, InT, 4, 4, 16, 256, 2, true>(j, s);
-    case 48:
-      return launch_poly_dma<TapT, InT, 4, 4, 8, 256, true>(j, s);
-    case 49:
-      return launch_poly_dma<TapT, InT, 4, 8, 8, 128, true>(j, s);
-    default:
+    case 8:
       return launch_poly<TapT, InT, 4, 4, 16, 256, MODE>(j, s);
+    case 24:
+      return launch_poly<TapT, InT, 4, 4, 16, 64, MODE, 0, true>(j, s);
+    case 28:
+      return launch_poly<TapT, InT, 4, 4, 16, 128, MODE, 0, true>(j, s);
+    default:
+      return hipErrorInvalidValue;
   }
 }
 
@@ -371,20 +205,14 @@ inline hipError_t launch_d4_int8(const FirJob& j, hipStream_t s) {
       return launch_poly<float, Iq8, 4, 8, 32, 128, kModeFir, 0, true>(j, s);
     case 5:
       return launch_poly<float, Iq8, 4, 4, 8, 256, kModeFir, 0, true>(j, s);
+    case 7:
+      return launch_generic<float, Iq8, kModeFir>(j, s);
     case 24:
       return launch_poly<float, Iq8, 4, 4, 16, 64, kModeFir, 0, true>(j, s);
-    case 27:
-      return launch_poly<float, Iq8, 4, 8, 16, 64, kModeFir, 0, true>(j, s);
     case 28:
       return launch_poly<float, Iq8, 4, 4, 16, 128, kModeFir, 0, true>(j, s);
-    case 50:
-      return launch_poly_cs<float, Iq8, 4, 8, 16, 256, 2, true>(j, s);
-    case 56:
-      return launch_poly_cs<float, Iq8, 4, 4, 16, 256, 2, true>(j, s);
-    case 57:
-      return launch_poly_cs<float, Iq8, 4, 8, 16, 128, 2, true>(j, s);
     default:
-      return launch_generic<float, Iq8, kModeFir>(j, s);
+      return hipErrorInvalidValue;
   }
 }
 

@@ -445,10 +445,9 @@ __device__ __forceinline__ void tile_epilogue(const FirParams& p, uint64_t out0,
 // Polyphase compute core shared by the polyphase kernels: thread t accumulates its R outputs from
 // the staged tile in LDS. JC = tap rows per chunk (a multiple of R); a chunk covers JC*D taps.
 // ------------------------------------------------------------------------------------------------
-template <class TapT, class InT, int D, int R, int JC, int WG, bool TAPS_LDS = false>
+template <class TapT, class InT, int D, int R, int JC, int WG>
 __device__ __forceinline__ void poly_compute(const float4* __restrict__ lds, const FirParams& p,
-                                             typename Product<TapT, InT>::type (&acc)[R],
-                                             const TapT* __restrict__ ltaps = nullptr) {
+                                             typename Product<TapT, InT>::type (&acc)[R]) {
   using Geo = TileGeo<InT, D, R, WG>;
   constexpr int G = Geo::G;
   constexpr int CPR = D / G;  // granule columns per input row
@@ -460,24 +459,13 @@ __device__ __forceinline__ void poly_compute(const float4* __restrict__ lds, con
     const float4* __restrict__ seg = lds + (t + c * (JC / R)) * Geo::SGP;
 #pragma unroll
     for (int h = 0; h < CPR; ++h) {
+      // taps first (one SMEM batch, one wait), then the LDS window (in-order, counted waits)
       TapT tv[JC][G];
-      if constexpr (TAPS_LDS) {
-        // zero-padded taps staged in LDS: wave-uniform (broadcast) reads, in order with the window
-        // reads, so the compiler can count lgkmcnt instead of draining it
-        const TapT* tp = ltaps + c * JC * D + h * G;
+      const TapBuf tb = tap_window<TapT>(p.taps, p.T, c * JC * D + h * G);
 #pragma unroll
-        for (int j = 0; j < JC; ++j) {
+      for (int j = 0; j < JC; ++j) {
 #pragma unroll
-          for (int e = 0; e < G; ++e) tv[j][e] = tp[j * D + e];
-        }
-      } else {
-        // taps first (one SMEM batch, one wait), then the LDS window (in-order, counted waits)
-        const TapBuf tb = tap_window<TapT>(p.taps, p.T, c * JC * D + h * G);
-#pragma unroll
-        for (int j = 0; j < JC; ++j) {
-#pragma unroll
-          for (int e = 0; e < G; ++e) tv[j][e] = tap_at<TapT>(tb, j * D + e);
-        }
+        for (int e = 0; e < G; ++e) tv[j][e] = tap_at<TapT>(tb, j * D + e);
       }
       float4 win[NWIN];
 #pragma unroll
@@ -497,25 +485,12 @@ __device__ __forceinline__ void poly_compute(const float4* __restrict__ lds, con
   }
 }
 
-// Stage taps [0, span) into LDS, zero past T. Callers barrier before use.
-template <class TapT, int WG>
-__device__ __forceinline__ void stage_taps(TapT* __restrict__ ltaps, const FirParams& p, uint32_t span) {
-  const TapT* __restrict__ taps = reinterpret_cast<const TapT*>(p.taps);
-  for (uint32_t i = threadIdx.x; i < span; i += WG) {
-    TapT v;
-    set_zero(v);
-    if (i < p.T) v = taps[i];
-    ltaps[i] = v;
-  }
-}
-
 // ------------------------------------------------------------------------------------------------
 // Kernel 1: polyphase-granule kernel, one tile per workgroup (D a multiple of the granule width G).
 // ABL (ablation, tuning probes only): 0 = full kernel, 1 = staging only, 2 = compute only.
 // NT: non-temporal (streaming) HBM loads for the staged input.
 // ------------------------------------------------------------------------------------------------
-template <class TapT, class InT, int D, int R, int JC, int WG, bool VEC, int MODE, int ABL = 0, bool NT = false,
-          bool TL = false>
+template <class TapT, class InT, int D, int R, int JC, int WG, bool VEC, int MODE, int ABL = 0, bool NT = false>
 __global__ __launch_bounds__(WG) void k_fir_poly(FirParams p) {
   using Geo = TileGeo<InT, D, R, WG>;
   using OutT = typename Product<TapT, InT>::type;
@@ -528,9 +503,7 @@ __global__ __launch_bounds__(WG) void k_fir_poly(FirParams p) {
   const uint64_t S0 = out0 * D;
   const uint32_t span = p.nch * JC * D;
   const uint32_t NG = ((Geo::KT - 1) * D + span + G - 1) / G;
-  // LDS: [tile granules | FM exchange (WG float2) | taps (span)]
-  TapT* ltaps = reinterpret_cast<TapT*>(lds + Geo::padded(NG - 1) + 1 + (WG * sizeof(float2) + 15) / 16);
-  if constexpr (TL) stage_taps<TapT, WG>(ltaps, p, span);
+  // LDS: [tile granules | FM exchange (WG float2)]
   if constexpr (ABL != 2) stage_tile<InT, Geo, WG, VEC, MODE, NT>(lds, in, S0, NG, p);
   __syncthreads();
 
@@ -542,7 +515,7 @@ __global__ __launch_bounds__(WG) void k_fir_poly(FirParams p) {
 #pragma unroll
     for (int r = 0; r < R; ++r) mac(acc[r], granule_sample<typename LdsSample<InT>::type>(v, r % G), 1.0f);
   } else {
-    poly_compute<TapT, InT, D, R, JC, WG, TL>(lds, p, acc, ltaps);
+    poly_compute<TapT, InT, D, R, JC, WG>(lds, p, acc);
   }
 
   float2* xs = reinterpret_cast<float2*>(lds + Geo::padded(NG - 1) + 1);
@@ -628,298 +601,6 @@ __global__ __launch_bounds__(WG) void k_fir_multi(FirParams p, MultiParams mp) {
     poly_compute<TapT, InT, D, R, JC, WG>(lds, pc, acc);
     tile_epilogue<MODE, OutT, R, WG>(pc, out0, acc, xs);
     __syncthreads();  // the next channel overwrites the tile
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
-// Kernel 1c: column-split polyphase kernel (D = 2G: two granule columns per row, e.g. complex D = 4).
-// Waves come in pairs over the same outputs: the even wave of a pair accumulates column 0 (phases
-// 0..G-1), the odd wave column 1. The column is wave-uniform, so a wave needs only NCH*JC*G taps --
-// 64 at T <= 128 -- which it loads into SGPRs once and keeps; the inner loop then issues nothing but
-// LDS window reads (in order, counted waits) and packed FMAs with SGPR tap operands. The odd wave
-// hands its partial sums to the even wave through a small LDS slab; the even wave stores.
-// ------------------------------------------------------------------------------------------------
-template <class TapT, class InT, int D, int R, int JC, int WG, int NCH, bool VEC, bool NT = false>
-__global__ __launch_bounds__(WG) void k_fir_poly_cs(FirParams p) {
-  constexpr int G = SampleT<InT>::kPerGranule;
-  static_assert(D == 2 * G, "two granule columns per row");
-  static_assert(WG % 128 == 0, "whole wave pairs");
-  constexpr int PAIRS = WG / 128;
-  using Geo = TileGeo<InT, D, R, PAIRS * 64>;  // one output segment per lane of a wave pair
-  using OutT = typename Product<TapT, InT>::type;
-  constexpr int NWIN = R + JC - 1;
-  static_assert(JC % R == 0, "chunk rows must be whole thread segments");
-
-  extern __shared__ __attribute__((aligned(16))) float4 lds[];
-  const InT* __restrict__ in = reinterpret_cast<const InT*>(p.in);
-  const uint64_t out0 = (uint64_t)blockIdx.x * p.tile_stride;
-  const uint64_t S0 = out0 * D;
-  const uint32_t span = NCH * JC * D;
-  const uint32_t NG = ((Geo::KT - 1) * D + span + G - 1) / G;
-  OutT* xs = reinterpret_cast<OutT*>(lds + Geo::padded(NG - 1) + 1);  // PAIRS*64*R partial sums
-
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t h = wave & 1u;          // this wave's granule column
-  const uint32_t pair = wave >> 1;
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t seg = pair * 64u + lane;  // output segment within the tile
-
-  // this wave's taps, once: t[(c*JC + j)*D + h*G + e]
-  TapT tv[NCH][JC][G];
-#pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-    const TapBuf tb = tap_window<TapT>(p.taps, p.T, c * JC * D + h * G);
-#pragma unroll
-    for (int j = 0; j < JC; ++j) {
-#pragma unroll
-      for (int e = 0; e < G; ++e) tv[c][j][e] = tap_at<TapT>(tb, j * D + e);
-    }
-  }
-
-  stage_tile<InT, Geo, WG, VEC, kModeFir, NT>(lds, in, S0, NG, p);
-  __syncthreads();
-
-  OutT acc[R];
-#pragma unroll
-  for (int r = 0; r < R; ++r) set_zero(acc[r]);
-#pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-    const float4* __restrict__ base = lds + (seg + c * (JC / R)) * Geo::SGP + h;
-    float4 win[NWIN];
-#pragma unroll
-    for (int u = 0; u < NWIN; ++u) {
-      const int q = u * 2;  // + h: even q and even SG keep the pad term independent of h
-      win[u] = base[q + Geo::PAD * (q / Geo::SG)];
-    }
-#pragma unroll
-    for (int j = 0; j < JC; ++j) {
-#pragma unroll
-      for (int e = 0; e < G; ++e) {
-#pragma unroll
-        for (int r = 0; r < R; ++r) mac(acc[r], granule_sample<typename LdsSample<InT>::type>(win[r + j], e), tv[c][j][e]);
-      }
-    }
-  }
-
-  if (h) {
-#pragma unroll
-    for (int r = 0; r < R; ++r) xs[r * PAIRS * 64 + seg] = acc[r];
-  }
-  __syncthreads();
-  if (!h) {
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const OutT o = xs[r * PAIRS * 64 + seg];
-      if constexpr (sizeof(OutT) == 8) {
-        acc[r].x += o.x;
-        acc[r].y += o.y;
-      } else {
-        acc[r] += o;
-      }
-    }
-    store_fir<OutT, R, NT>(reinterpret_cast<OutT*>(p.out), out0 + seg * R, p.N, acc);
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
-// Kernel 1p: the polyphase kernel as a persistent, software-pipelined loop. Each workgroup walks
-// tiles blockIdx.x, blockIdx.x + gridDim.x, ...; while it computes tile i out of LDS, the HBM loads
-// of tile i+1 are already in flight into registers (non-temporal: the input is read exactly once),
-// so every workgroup overlaps its own streaming with its own FMAs and the CU keeps 4 such
-// workgroups (16 waves) resident. HALO = granules per thread reserved for the tile's halo
-// (span - D samples past the tile body); the host only selects this kernel when they fit.
-// ------------------------------------------------------------------------------------------------
-template <class InT, int SG, int HALO>
-struct TileRegs {
-  float4 body[SG];
-  float4 halo[HALO];
-};
-
-// Non-temporal 16-byte buffer load: one SGPR descriptor + one VGPR offset for the whole tile
-// (flat loads would need a 64-bit address per load: +2 VGPRs each, which the pipeline cannot afford).
-typedef float gsdr_bf32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ float4 buffer_load16_nt(__amdgpu_buffer_rsrc_t rsrc, uint32_t voff, uint32_t soff) {
-  const gsdr_bf32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)voff, (int)soff, 2 /* nt */);
-  return make_float4(v.x, v.y, v.z, v.w);
-}
-
-// Issue the HBM loads of one tile into registers and return without waiting for them. The
-// descriptor's range covers only the whole granules that exist, so granules past the input's end
-// read as zero without per-granule branches; pipe_store rewrites the one granule that straddles the
-// end (odd sample count) after the fact.
-template <class InT, class Geo, int WG, int HALO>
-__device__ __forceinline__ void pipe_load(TileRegs<InT, Geo::SG, HALO>& r, const InT* __restrict__ in, uint64_t S0,
-                                          uint32_t NG, const FirParams& p) {
-  constexpr int G = Geo::G;
-  const uint32_t tid = threadIdx.x;
-  const uint64_t avail = p.L > S0 ? p.L - S0 : 0;  // samples readable from S0
-  const uint32_t nrec = avail >= (uint64_t)NG * G ? NG * 16u : (uint32_t)(avail / G) * 16u;
-  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(in + S0), (short)0, (int)nrec,
-                                                                       0x00020000);
-#pragma unroll
-  for (int k = 0; k < Geo::SG; ++k) r.body[k] = buffer_load16_nt(rsrc, tid * 16u, (uint32_t)(k * WG * 16));
-#pragma unroll
-  for (int k = 0; k < HALO; ++k) {
-    r.halo[k] = buffer_load16_nt(rsrc, tid * 16u, (uint32_t)((Geo::SG + k) * WG * 16));
-  }
-}
-
-template <class InT, class Geo, int WG, int HALO, int MODE>
-__device__ __forceinline__ void pipe_store(float4* __restrict__ lds, const TileRegs<InT, Geo::SG, HALO>& r,
-                                           const InT* __restrict__ in, uint64_t S0, uint32_t NG, const FirParams& p) {
-  constexpr int G = Geo::G;
-  const uint32_t tid = threadIdx.x;
-  const uint32_t s0 = (uint32_t)S0;
-#pragma unroll
-  for (int k = 0; k < Geo::SG; ++k) {
-    const uint32_t g = k * WG + tid;
-    lds[Geo::padded(g)] = stage_transform<InT, MODE>(r.body[k], s0 + g * G, p);
-  }
-#pragma unroll
-  for (int k = 0; k < HALO; ++k) {
-    const uint32_t g = (Geo::SG + k) * WG + tid;
-    if (g < NG) lds[Geo::padded(g)] = stage_transform<InT, MODE>(r.halo[k], s0 + g * G, p);
-  }
-  const uint64_t avail = p.L > S0 ? p.L - S0 : 0;
-  if (avail < (uint64_t)NG * G && avail % G != 0) {  // wave-uniform: only the input's last tile
-    const uint32_t gl = (uint32_t)(avail / G);        // the straddling granule
-    if (gl % WG == tid) {
-      lds[Geo::padded(gl)] = stage_transform<InT, MODE>(load_granule<InT, false>(in, S0 + (uint64_t)gl * G, p.L),
-                                                        s0 + gl * G, p);
-    }
-  }
-}
-
-template <class TapT, class InT, int D, int R, int JC, int WG, int HALO, int MODE>
-__global__ __launch_bounds__(WG, 4) void k_fir_poly_pipe(FirParams p, uint32_t ntiles) {
-  using Geo = TileGeo<InT, D, R, WG>;
-  using OutT = typename Product<TapT, InT>::type;
-  constexpr int G = Geo::G;
-
-  extern __shared__ __attribute__((aligned(16))) float4 lds[];
-  const InT* __restrict__ in = reinterpret_cast<const InT*>(p.in);
-  const uint32_t span = p.nch * JC * D;
-  const uint32_t NG = ((Geo::KT - 1) * D + span + G - 1) / G;
-  float2* xs = reinterpret_cast<float2*>(lds + Geo::padded(NG - 1) + 1);
-
-  uint32_t tile = blockIdx.x;
-  if (tile >= ntiles) return;
-  TileRegs<InT, Geo::SG, HALO> regs;
-  pipe_load<InT, Geo, WG, HALO>(regs, in, (uint64_t)tile * p.tile_stride * D, NG, p);
-  for (;;) {
-    const uint64_t out0 = (uint64_t)tile * p.tile_stride;
-    pipe_store<InT, Geo, WG, HALO, MODE>(lds, regs, in, out0 * D, NG, p);
-    __syncthreads();
-    const uint32_t next = tile + gridDim.x;
-    if (next < ntiles) pipe_load<InT, Geo, WG, HALO>(regs, in, (uint64_t)next * p.tile_stride * D, NG, p);
-    OutT acc[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) set_zero(acc[r]);
-    poly_compute<TapT, InT, D, R, JC, WG>(lds, p, acc);
-    tile_epilogue<MODE, OutT, R, WG>(p, out0, acc, xs);
-    if (next >= ntiles) break;
-    __syncthreads();  // every wave is done reading this tile before the next one overwrites it
-    tile = next;
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
-// Kernel 1d: persistent, double-buffered LDS-DMA pipeline (FIR mode). HBM -> LDS with
-// buffer_load_dwordx4 ... lds (no VGPR round trip, no ds_write): while a workgroup computes tile i
-// out of one LDS buffer, its waves' DMA for tile i+1 fills the other. The DMA is issued from inline
-// asm so the compiler does not serialise every ds_read behind it (its waitcnt pass cannot tell the
-// two buffers apart); completion is awaited by hand: s_waitcnt vmcnt(0), then the barrier.
-// Pad slots of the padded layout and granules past the input's end are fetched from an
-// out-of-range offset, which the buffer range check turns into zeros.
-// ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t lds_byte_addr(const void* p) {
-  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
-}
-
-__device__ __forceinline__ void dma16_nt(uint32_t lds_base, uint32_t voff, gsdr_v4i32 rsrc) {
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %3\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %1, %2, 0 offen nt lds\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(voff), "s"(rsrc), "s"(lds_base)
-      : "memory");
-}
-
-template <int SG, int SGP>
-__device__ __forceinline__ uint32_t slot_source_offset(uint32_t s, uint32_t NGP) {
-  const uint32_t seg = s / SGP;
-  const uint32_t w = s - seg * SGP;
-  return (w < (uint32_t)SG && s < NGP) ? (seg * SG + w) * 16u : 0x80000000u;
-}
-
-template <class InT, class Geo, int WG>
-__device__ __forceinline__ void dma_tile(float4* buf, uint32_t slots, const InT* __restrict__ in, uint64_t S0,
-                                         uint32_t NG, uint32_t NGP, const FirParams& p) {
-  constexpr int G = Geo::G;
-  const uint64_t avail = p.L > S0 ? p.L - S0 : 0;
-  const uint32_t nrec = avail >= (uint64_t)NG * G ? NG * 16u : (uint32_t)(avail / G) * 16u;
-  const uint64_t a = reinterpret_cast<uint64_t>(in + S0);
-  const gsdr_v4i32 rsrc = gsdr_v4i32{(int)(uint32_t)a, (int)(uint32_t)(a >> 32) & 0xffff, (int)nrec, 0x00020000};
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t base = lds_byte_addr(buf) + wave * 64u * 16u;
-  for (uint32_t k = 0; k < slots; k += WG) {
-    const uint32_t s = k + wave * 64u + lane;
-    dma16_nt(base + k * 16u, slot_source_offset<Geo::SG, Geo::SGP>(s, NGP), rsrc);
-  }
-}
-
-// The one granule that straddles the input's end (odd sample count) is not whole, so the range
-// check zeroed it; rewrite it from memory (last tile only). Caller barriers after.
-template <class InT, class Geo, int WG>
-__device__ __forceinline__ bool dma_fixup(float4* buf, const InT* __restrict__ in, uint64_t S0, uint32_t NG,
-                                          const FirParams& p) {
-  constexpr int G = Geo::G;
-  const uint64_t avail = p.L > S0 ? p.L - S0 : 0;
-  if (!(avail < (uint64_t)NG * G && avail % G != 0)) return false;
-  const uint32_t gl = (uint32_t)(avail / G);
-  if (gl % WG == threadIdx.x) buf[Geo::padded(gl)] = load_granule<InT, false>(in, S0 + (uint64_t)gl * G, p.L);
-  return true;
-}
-
-template <class TapT, class InT, int D, int R, int JC, int WG, bool TL = false>
-__global__ __launch_bounds__(WG) void k_fir_poly_dma(FirParams p, uint32_t ntiles, uint32_t slots) {
-  using Geo = TileGeo<InT, D, R, WG>;
-  using OutT = typename Product<TapT, InT>::type;
-  constexpr int G = Geo::G;
-  extern __shared__ __attribute__((aligned(16))) float4 lds[];
-  const InT* __restrict__ in = reinterpret_cast<const InT*>(p.in);
-  const uint32_t span = p.nch * JC * D;
-  const uint32_t NG = ((Geo::KT - 1) * D + span + G - 1) / G;
-  const uint32_t NGP = Geo::padded(NG - 1) + 1;
-  TapT* ltaps = reinterpret_cast<TapT*>(lds + 2 * slots);
-
-  uint32_t tile = blockIdx.x;
-  if (tile >= ntiles) return;
-  if constexpr (TL) stage_taps<TapT, WG>(ltaps, p, span);
-  dma_tile<InT, Geo, WG>(lds, slots, in, (uint64_t)tile * p.tile_stride * D, NG, NGP, p);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (dma_fixup<InT, Geo, WG>(lds, in, (uint64_t)tile * p.tile_stride * D, NG, p)) __syncthreads();
-  for (uint32_t it = 0;; ++it) {
-    float4* cur = lds + (it & 1u) * slots;
-    float4* nxt = lds + ((it + 1u) & 1u) * slots;
-    const uint32_t next = tile + gridDim.x;
-    if (next < ntiles) dma_tile<InT, Geo, WG>(nxt, slots, in, (uint64_t)next * p.tile_stride * D, NG, NGP, p);
-    OutT acc[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) set_zero(acc[r]);
-    poly_compute<TapT, InT, D, R, JC, WG, TL>(cur, p, acc, ltaps);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of the next tile has landed
-    tile_epilogue<kModeFir, OutT, R, WG>(p, (uint64_t)tile * p.tile_stride, acc, nullptr);
-    __syncthreads();  // every wave's DMA landed, and nobody still reads `cur`
-    if (next >= ntiles) break;
-    if (dma_fixup<InT, Geo, WG>(nxt, in, (uint64_t)next * p.tile_stride * D, NG, p)) __syncthreads();
-    tile = next;
   }
 }
 
@@ -1019,12 +700,12 @@ __global__ __launch_bounds__(256) void k_fir_generic(FirParams p) {
 // Host-side sizing helpers
 // ------------------------------------------------------------------------------------------------
 template <class InT, int D, int R, int WG>
-constexpr size_t poly_lds_bytes(uint32_t span_samples, int mode, size_t tap_bytes = 0) {
+constexpr size_t poly_lds_bytes(uint32_t span_samples, int mode) {
   using Geo = TileGeo<InT, D, R, WG>;
   const uint32_t NG = ((Geo::KT - 1) * D + span_samples + Geo::G - 1) / Geo::G;
   size_t bytes = (size_t)(Geo::padded(NG - 1) + 1) * 16u;
-  if (mode != kModeFir || tap_bytes) bytes += ((size_t)WG * sizeof(float2) + 15) / 16 * 16;
-  return bytes + tap_bytes;
+  if (mode != kModeFir) bytes += ((size_t)WG * sizeof(float2) + 15) / 16 * 16;
+  return bytes;
 }
 
 }  // namespace gsdr

@@ -110,7 +110,7 @@ def test_fir_restores_current_device(cuda):
     assert torch.cuda.current_device() == 0
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 20, 21, 22, 23, 24, 25, 26, 27, 30, 31, 32, 33, 40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 53, 54, 55, 56])
+@pytest.mark.parametrize("variant", [0, 1, 3, 4, 5, 7, 8, 24, 28])
 def test_fir_fc_d4_variants(cuda, variant):
     """Every tile shape of the headline kernel (gsdrxFirFCVariant) meets the same bar."""
     from gsdr_amd import ops

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Tuning probe for the headline FIR (FC, D=4, T=127, 2^24 outputs): times gsdrxFirFCVariant tile
-shapes and ablations (variants >= 100, see gsdr_amd/csrc/fir_probe.hip) interleaved in one process,
+shapes and ablations (variants >= 100, see launch_fc_probe in gsdr_amd/csrc/fir.hip) interleaved in one process,
 HIP events on the launch stream. Development tool; not part of the library."""
 import argparse
 import os
@@ -18,7 +18,7 @@ L = (N - 1) * D + TAPS
 BYTES = 8 * L + 8 * N + 4 * TAPS
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--variants", default="0,1,2,3,4,5,6,100,101,102")
+ap.add_argument("--variants", default="0,1,3,4,5,8,24,28,104,107,111")
 ap.add_argument("--reps", type=int, default=20)
 ap.add_argument("--rounds", type=int, default=3)
 ap.add_argument("--fm", action="store_true", help="also time the fused FM chain")

@@ -20,7 +20,7 @@ L = (N - 1) * D + TAPS
 BYTES = 8 * L + 8 * N + 4 * TAPS
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--variants", default="0,1,107,111")
+ap.add_argument("--variants", default="0,8,104,107,111")
 ap.add_argument("--launches", type=int, default=400)
 ap.add_argument("--window", type=int, default=50)
 ap.add_argument("--cool", type=float, default=2.0, help="idle seconds before each variant")

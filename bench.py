@@ -229,6 +229,21 @@ def secondary_configs(torch, ops, device, taps):
                        "alg_gbps": round(b / t / 1e9, 1), "alg_bytes_per_launch": b,
                        "fma_tflops": round(4 * TAPS * N_OUT / t / 1e12, 1)}
     del x8s, yf
+    # true recursive IIR: 4th-order Butterworth over 2^24 samples
+    from scipy import signal as sps
+
+    bb, aa = (torch.tensor(v, dtype=torch.float32, device=device) for v in sps.butter(4, 0.1))
+    for dt, name, nbytes in ((torch.float32, "gsdrIirFF", 4), (torch.complex64, "gsdrIirCC", 8)):
+        n = 1 << 24
+        xi = torch.rand(n, dtype=dt, device=device, generator=g)
+        yi = torch.empty_like(xi)
+        argsets = [(bb.data_ptr(), aa.data_ptr(), 5, None, None, xi.data_ptr(), yi.data_ptr(), n, device.index, stream)]
+        t = time_abi(torch, getattr(abi.lib, name), argsets, reps=20, settle=100)
+        out[f"iir_{'cc' if dt == torch.complex64 else 'ff'}"] = {
+            "config": f"{name}, 4th-order Butterworth (K = 5), 2^24 samples, parallel scan",
+            "us_per_launch": round(t * 1e6, 2), "msamples_per_s": round(n / t / 1e6, 1),
+            "alg_gbps": round(2 * nbytes * n / t / 1e9, 1)}
+        del xi, yi
     reps = 50
     n = 1 << 24
     ops.qpsk256_init(0, 1.0, device.index)

@@ -54,6 +54,11 @@ SIGNATURES = {
     "gsdrMultiplyCF": (_err, [_p, _p, _p, _sz, _i32, _p]),
     "gsdrAddToMagnitude": (_err, [_p, _f, _p, _sz, _i32, _p]),
     "gsdrAbs": (_err, [_p, _p, _sz, _i32, _p]),
+    # iir.h
+    "gsdrIirFF": (_err, [_p, _p, _sz, _p, _p, _p, _p, _sz, _i32, _p]),
+    "gsdrIirCC": (_err, [_p, _p, _sz, _p, _p, _p, _p, _sz, _i32, _p]),
+    "gsdrIirFFCustom": (_err, [_p, _p, _sz, _p, _p, _p, _p, _sz, _sz, _i32, _p]),
+    "gsdrIirCCCustom": (_err, [_p, _p, _sz, _p, _p, _p, _p, _sz, _sz, _i32, _p]),
     # trig.h / conversion.h
     "gsdrCosineC": (_err, [_f, _f, _p, _sz, _i32, _p]),
     "gsdrCosineF": (_err, [_f, _f, _p, _sz, _i32, _p]),

@@ -1,0 +1,480 @@
+// gsdr-mi355x: IIR filter as a true recursive filter (include/gsdr/iir.h; SURVEY.md section 8(f)
+// row 4). Replaces reference src/iir.cu, whose kernel restarts every thread's 8-sample chunk from
+// zero state (iir.cu:121-127) and ignores the history arguments (iir.cu:213-214).
+//
+//   y[n] = sum_{i<=P} b[i] x[n-i] - sum_{1<=i<=P} a[i] y[n-i],   P = K - 1
+//
+// Parallel scan over the linear recursion (state s = (y[n-1], ..., y[n-P])):
+//   1. k_iir_chunks<kTails>: the signal is cut into 32-sample chunks (a workgroup stages WG chunks
+//      through LDS for coalesced HBM access); each thread filters its chunk from zero output state
+//      (the FIR part sees the true previous inputs) and stores the chunk's zero-state tail T_c.
+//   2. The true state entering chunk c obeys S_{c+1} = M S_c + T_c, M = the P x P transition over a
+//      chunk of the homogeneous recursion (k_iir_setup, with its powers M^(G^k)). That affine
+//      recurrence is scanned hierarchically in groups of 64 elements, one wave per group and one
+//      element per lane: up-sweep = Hillis-Steele scan within the wave (6 steps with M^(2^s)),
+//      whose last lane is the group aggregate for the next level; down-sweep = every element's start
+//      state M^r S_group + prefix_(r-1) at once (table of M^r, r < 64, per level).
+//   3. k_iir_chunks<kFinal>: each chunk re-runs from its true start state and writes y.
+//   4. k_iir_history: the caller's history buffers receive the last P inputs / outputs.
+// State, scan and matrices are double (see Acc below); complex samples with real coefficients are
+// two independent recursions sharing M. State dimensions are padded to a compiled P (zero
+// coefficients beyond K-1 leave the recursion unchanged).
+#include <hip/hip_runtime.h>
+
+#include "gsdr/iir.h"
+#include "launch.hpp"
+
+namespace gsdr {
+namespace iir {
+
+constexpr int kChunk = 32;  // samples per level-0 chunk (>= the largest P)
+constexpr int kGroup = 64;  // scan elements per group = one wave, one element per lane
+constexpr int kMaxLevels = 8;
+
+// The recursion state, the scan and the transition matrices are kept in double: the direct form
+// amplifies an inconsistent perturbation of its P-sample state by 10^2..10^3 (tests/test_gpu_iir.py),
+// and rounding a scanned state to float32 at every chunk boundary is exactly such a perturbation.
+// Samples stay float32 in HBM and LDS; only the outputs are rounded.
+template <class S>
+struct Acc;
+template <>
+struct Acc<float> {
+  using type = double;
+};
+template <>
+struct Acc<float2> {
+  using type = double2;
+};
+
+__device__ __forceinline__ float zero_s(float) { return 0.0f; }
+__device__ __forceinline__ float2 zero_s(float2) { return make_float2(0.0f, 0.0f); }
+__device__ __forceinline__ double zero_s(double) { return 0.0; }
+__device__ __forceinline__ double2 zero_s(double2) { return make_double2(0.0, 0.0); }
+__device__ __forceinline__ double fma_s(double c, double x, double acc) { return fma(c, x, acc); }
+__device__ __forceinline__ double2 fma_s(double c, double2 x, double2 acc) {
+  return make_double2(fma(c, x.x, acc.x), fma(c, x.y, acc.y));
+}
+__device__ __forceinline__ double fma_s(double c, float x, double acc) { return fma(c, (double)x, acc); }
+__device__ __forceinline__ double2 fma_s(double c, float2 x, double2 acc) {
+  return make_double2(fma(c, (double)x.x, acc.x), fma(c, (double)x.y, acc.y));
+}
+__device__ __forceinline__ double to_acc(float v) { return (double)v; }
+__device__ __forceinline__ double2 to_acc(float2 v) { return make_double2(v.x, v.y); }
+__device__ __forceinline__ float to_sample(double v) { return (float)v; }
+__device__ __forceinline__ float2 to_sample(double2 v) { return make_float2((float)v.x, (float)v.y); }
+__device__ __forceinline__ double add_s(double a, double b) { return a + b; }
+__device__ __forceinline__ double shfl_up_s(double v, int d) { return __shfl_up(v, d, 64); }
+__device__ __forceinline__ double2 shfl_up_s(double2 v, int d) {
+  return make_double2(__shfl_up(v.x, d, 64), __shfl_up(v.y, d, 64));
+}
+__device__ __forceinline__ double2 add_s(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
+
+struct Coeffs {
+  const float* b;
+  const float* a;
+  int K;
+};
+
+// coefficient i of a zero-padded array (uniform: the compiler turns these into scalar loads)
+__device__ __forceinline__ double coeff(const float* c, int K, int i) { return i < K ? (double)c[i] : 0.0; }
+
+enum ChunkPass : int { kTails = 0, kFinal = 1 };
+
+// x[n] for n >= -P: the input, or the caller's input history (K-1 entries) for n < 0, else zero
+template <class S>
+__device__ __forceinline__ S x_at(const S* __restrict__ x, const S* __restrict__ xh, int K, int64_t n) {
+  if (n >= 0) return x[n];
+  return (xh && -1 - n < K - 1) ? xh[-1 - n] : zero_s(S{});
+}
+
+// matrix product C = A * B (P x P, row-major) by a workgroup: each thread computes entries
+template <int P>
+__device__ __forceinline__ void mat_mul(const double* __restrict__ A, const double* __restrict__ B,
+                                        double* __restrict__ C, int t, int nt) {
+  for (int e = t; e < P * P; e += nt) {
+    const int i = e / P, j = e % P;
+    double acc = 0.0;
+#pragma unroll
+    for (int l = 0; l < P; ++l) acc = fma(A[i * P + l], B[l * P + j], acc);
+    C[e] = acc;
+  }
+}
+
+// One workgroup prepares the scan's constants:
+//   s0        = entry state (double) from the caller's output history, zero-padded to P;
+//   T[k][r]   = M_k^r for r in [0, 64), with M_0 the transition over one chunk (column j = state after
+//               kChunk steps of y[n] = -sum a[i] y[n-i] from e_j) and M_{k+1} = M_k^64,
+// for every level k = 0..levels. Each level's table is built by doubling in `work` (LDS when it fits,
+// else the global table itself): T[h] = T[h/2]^2, then T[h + q] = T[h] T[q].
+// barrier for the setup workgroup; the device-scope fence is needed only when the table lives in
+// global memory (it costs ~1 us, and the doubling rounds need ~50 barriers)
+__device__ __forceinline__ void sync_table(const double* work) {
+  if (!work) __threadfence();
+  __syncthreads();
+}
+
+template <class S, int P, int NT>
+__device__ void iir_setup(const Coeffs& cf, const S* __restrict__ yh, typename Acc<S>::type* __restrict__ s0,
+                          double* __restrict__ T, int levels, double* __restrict__ work) {
+  const int t = threadIdx.x;
+  const int Pk = cf.K - 1;
+  constexpr int PP = P * P;
+  if (t < P) s0[t] = (yh && t < Pk) ? to_acc(yh[t]) : zero_s(typename Acc<S>::type{});
+  for (int lv = 0; lv <= levels; ++lv) {
+    double* __restrict__ W = work ? work : T + (size_t)lv * kGroup * PP;
+    if (lv == 0) {
+      if (t < P) {  // M_0, column t
+        double am[P + 1];
+#pragma unroll
+        for (int i = 0; i <= P; ++i) am[i] = -coeff(cf.a, cf.K, i);
+        double ys[P];
+#pragma unroll
+        for (int i = 0; i < P; ++i) ys[i] = i == t ? 1.0 : 0.0;
+        for (int k = 0; k < kChunk; ++k) {
+          double acc = 0.0;
+#pragma unroll
+          for (int i = 1; i <= P; ++i) acc = fma(am[i], ys[i - 1], acc);
+#pragma unroll
+          for (int i = P - 1; i > 0; --i) ys[i] = ys[i - 1];
+          ys[0] = acc;
+        }
+#pragma unroll
+        for (int i = 0; i < P; ++i) W[PP + i * P + t] = ys[i];
+      }
+    } else {  // M_lv = M_{lv-1}^64 = (M_{lv-1}^32)^2, from the previous level's table
+      const double* Tp = work ? work : T + (size_t)(lv - 1) * kGroup * PP;
+      double m2[(PP + NT - 1) / NT];
+      int c = 0;
+      for (int e = t; e < PP; e += NT, ++c) {
+        const int i = e / P, j = e % P;
+        double acc = 0.0;
+#pragma unroll
+        for (int l = 0; l < P; ++l) acc = fma(Tp[32 * PP + i * P + l], Tp[32 * PP + l * P + j], acc);
+        m2[c] = acc;
+      }
+      sync_table(work);
+      c = 0;
+      for (int e = t; e < PP; e += NT, ++c) W[PP + e] = m2[c];
+    }
+    for (int e = t; e < PP; e += NT) W[e] = (e / P == e % P) ? 1.0 : 0.0;
+    sync_table(work);
+    for (int h = 2; h < kGroup; h *= 2) {
+      mat_mul<P>(W + (h / 2) * PP, W + (h / 2) * PP, W + h * PP, t, NT);
+      sync_table(work);
+      for (int w = t; w < (h - 1) * PP; w += NT) {
+        const int q = 1 + w / PP, e = w % PP;
+        if (h + q < kGroup) {
+          const int i = e / P, j = e % P;
+          double acc = 0.0;
+#pragma unroll
+          for (int l = 0; l < P; ++l) acc = fma(W[h * PP + i * P + l], W[q * PP + l * P + j], acc);
+          W[(h + q) * PP + e] = acc;
+        }
+      }
+      sync_table(work);
+    }
+    if (work) {  // publish the level's table
+      double* Tl = T + (size_t)lv * kGroup * PP;
+      for (int e = t; e < kGroup * PP; e += NT) Tl[e] = W[e];
+      __syncthreads();
+    }
+  }
+}
+
+// Workgroup of WG threads = WG consecutive chunks = one tile of WG * kChunk samples, staged through
+// LDS so HBM sees coalesced loads/stores; thread t runs the recursion over its chunk from the tile
+// (chunk stride kChunk + 1 elements: consecutive lanes land on different banks).
+template <class S>
+struct TileShape {
+  static constexpr int WG = sizeof(S) == 4 ? 256 : 128;  // 33 KB of LDS either way
+  static constexpr int TS = WG * kChunk;
+  static constexpr int STRIDE = kChunk + 1;
+  __device__ static int at(int idx) { return idx + idx / kChunk; }
+};
+
+struct SetupArgs {
+  const void* yh;
+  void* s0;
+  double* T;
+  int levels;
+};
+
+template <int P>
+constexpr bool kTableInLds = kGroup * P * P * sizeof(double) <= 32 * 1024;
+
+template <class S, int P, int PASS>
+__global__ __launch_bounds__(TileShape<S>::WG) void k_iir_chunks(Coeffs cf, const S* __restrict__ x,
+                                                                 const S* __restrict__ xh, uint64_t n,
+                                                                 const typename Acc<S>::type* __restrict__ starts,
+                                                                 typename Acc<S>::type* __restrict__ tails,
+                                                                 S* __restrict__ y, SetupArgs setup) {
+  using TSh = TileShape<S>;
+  using A = typename Acc<S>::type;
+  constexpr size_t kTileBytes = sizeof(S) * TSh::WG * TSh::STRIDE;
+  constexpr size_t kTableBytes = kTableInLds<P> ? kGroup * P * P * sizeof(double) : 0;
+  __shared__ __attribute__((aligned(16))) char smem[kTileBytes > kTableBytes ? kTileBytes : kTableBytes];
+  S* tile = reinterpret_cast<S*>(smem);
+  const int t = threadIdx.x;
+  if constexpr (PASS == kTails) {
+    // the extra last workgroup builds the scan constants while the others compute the tails
+    if (blockIdx.x == gridDim.x - 1) {
+      iir_setup<S, P, TSh::WG>(cf, static_cast<const S*>(setup.yh), static_cast<A*>(setup.s0), setup.T, setup.levels,
+                               kTableInLds<P> ? reinterpret_cast<double*>(smem) : nullptr);
+      return;
+    }
+  }
+  const uint64_t base = (uint64_t)blockIdx.x * TSh::TS;
+  const uint32_t tlen = n - base < (uint64_t)TSh::TS ? (uint32_t)(n - base) : (uint32_t)TSh::TS;
+  for (int idx = t; idx < (int)tlen; idx += TSh::WG) tile[TSh::at(idx)] = x[base + idx];
+  __syncthreads();
+  const uint64_t c = (uint64_t)blockIdx.x * TSh::WG + t;
+  const uint64_t n0 = c * kChunk;
+  if (n0 < n) {
+    const uint32_t len = n - n0 < (uint64_t)kChunk ? (uint32_t)(n - n0) : (uint32_t)kChunk;
+    double b[P + 1], am[P + 1];
+#pragma unroll
+    for (int i = 0; i <= P; ++i) {
+      b[i] = coeff(cf.b, cf.K, i);
+      am[i] = -coeff(cf.a, cf.K, i);
+    }
+    S xs[P];  // x[n-1-i] (exact floats)
+    A ys[P];  // y[n-1-i]
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+      xs[i] = x_at(x, xh, cf.K, (int64_t)n0 - 1 - i);
+      ys[i] = PASS == kFinal ? starts[c * P + i] : zero_s(A{});
+    }
+    S* __restrict__ row = tile + t * TSh::STRIDE;
+    for (uint32_t k = 0; k < len; ++k) {
+      const S xv = row[k];
+      A acc = fma_s(b[0], xv, zero_s(A{}));
+#pragma unroll
+      for (int i = 1; i <= P; ++i) acc = fma_s(b[i], xs[i - 1], acc);
+#pragma unroll
+      for (int i = 1; i <= P; ++i) acc = fma_s(am[i], ys[i - 1], acc);
+#pragma unroll
+      for (int i = P - 1; i > 0; --i) {
+        xs[i] = xs[i - 1];
+        ys[i] = ys[i - 1];
+      }
+      xs[0] = xv;
+      ys[0] = acc;
+      if constexpr (PASS == kFinal) row[k] = to_sample(acc);  // y replaces x in this thread's row
+    }
+    if constexpr (PASS == kTails) {
+#pragma unroll
+      for (int i = 0; i < P; ++i) tails[c * P + i] = ys[i];
+    } else if (n0 + len == n) {
+      // the last chunk's state after the call (outputs, then inputs, newest first), staged for the
+      // caller's history buffers
+#pragma unroll
+      for (int i = 0; i < P; ++i) {
+        tails[i] = ys[i];
+        tails[P + i] = to_acc(xs[i]);
+      }
+    }
+  }
+  if constexpr (PASS == kFinal) {
+    __syncthreads();
+    for (int idx = t; idx < (int)tlen; idx += TSh::WG) y[base + idx] = tile[TSh::at(idx)];
+  }
+}
+
+// Up-sweep of one level: wave g scans its 64 elements (lane r = element j0 + r) from zero state,
+// Hillis-Steele over the affine composition: v_r <- v_r + M^(2^s) v_(r-2^s). Lane r's result is the
+// zero-state prefix through element r (kept in `incl` for the down-sweep); lane 63's is the group
+// aggregate for the next level.
+template <class A, int P>
+__global__ __launch_bounds__(64) void k_iir_up(const A* __restrict__ elems, uint64_t E, const double* __restrict__ T,
+                                               A* __restrict__ incl, A* __restrict__ aggs) {
+  constexpr int PP = P * P;
+  const uint64_t g = blockIdx.x;
+  const int r = threadIdx.x;
+  const uint64_t j = g * kGroup + r;
+  const uint64_t last = (E - 1 < g * kGroup + kGroup - 1) ? E - 1 - g * kGroup : kGroup - 1;
+  A v[P];
+#pragma unroll
+  for (int i = 0; i < P; ++i) v[i] = j < E ? elems[j * P + i] : zero_s(A{});
+#pragma unroll
+  for (int s = 0; s < 6; ++s) {
+    const int d = 1 << s;
+    const double* __restrict__ Md = T + (size_t)d * PP;
+    A w[P];
+#pragma unroll
+    for (int i = 0; i < P; ++i) w[i] = shfl_up_s(v[i], d);
+    if (r >= d) {
+#pragma unroll
+      for (int i = 0; i < P; ++i) {
+        A acc = v[i];
+#pragma unroll
+        for (int l = 0; l < P; ++l) acc = fma_s(Md[i * P + l], w[l], acc);
+        v[i] = acc;
+      }
+    }
+  }
+  if (j < E) {
+#pragma unroll
+    for (int i = 0; i < P; ++i) incl[j * P + i] = v[i];
+  }
+  if (aggs && (uint64_t)r == last) {
+#pragma unroll
+    for (int i = 0; i < P; ++i) aggs[g * P + i] = v[i];
+  }
+}
+
+// Down-sweep of one level: element j = g*64 + r starts in state M^r S_g + prefix_(r-1), with S_g the
+// group's start state (group_starts[g], or s0 at the top level) and prefix the up-sweep's inclusive
+// zero-state prefix of the previous lane. Overwrites incl with the start states.
+template <class A, int P>
+__global__ __launch_bounds__(64) void k_iir_down(uint64_t E, const double* __restrict__ T,
+                                                 const A* __restrict__ group_starts, const A* __restrict__ s0,
+                                                 A* __restrict__ incl_starts) {
+  constexpr int PP = P * P;
+  const uint64_t g = blockIdx.x;
+  const int r = threadIdx.x;
+  const uint64_t j = g * kGroup + r;
+  A pre[P], sg[P];
+#pragma unroll
+  for (int i = 0; i < P; ++i) {
+    const A mine = j < E ? incl_starts[j * P + i] : zero_s(A{});
+    pre[i] = shfl_up_s(mine, 1);
+    sg[i] = group_starts ? group_starts[g * P + i] : s0[i];
+  }
+  if (j >= E) return;
+  const double* __restrict__ Mr = T + (size_t)r * PP;
+#pragma unroll
+  for (int i = 0; i < P; ++i) {
+    A acc = r > 0 ? pre[i] : zero_s(A{});
+#pragma unroll
+    for (int l = 0; l < P; ++l) acc = fma_s(Mr[i * P + l], sg[l], acc);
+    incl_starts[j * P + i] = acc;
+  }
+}
+
+// The caller's history buffers after the call, from the state staged by the last chunk.
+template <class S>
+__global__ __launch_bounds__(64) void k_iir_history(S* __restrict__ xh, S* __restrict__ yh,
+                                                    const typename Acc<S>::type* __restrict__ st, int P, int Pk) {
+  const int i = threadIdx.x;
+  if (i < Pk) {
+    if (yh) yh[i] = to_sample(st[i]);
+    if (xh) xh[i] = to_sample(st[P + i]);
+  }
+}
+
+template <class S, int P>
+static hipError_t run(const Coeffs& cf, S* xh, S* yh, const S* x, S* y, uint64_t n, hipStream_t st) {
+  using A = typename Acc<S>::type;
+  const uint64_t C = ceil_div<uint64_t>(n, kChunk);
+  // level sizes: E[0] = C chunks, E[k+1] = ceil(E[k] / G) until one group remains
+  constexpr uint64_t G = kGroup;
+  uint64_t E[kMaxLevels + 1];
+  int levels = 0;
+  E[0] = C;
+  while (E[levels] > G) {
+    if (levels == kMaxLevels) return hipErrorInvalidValue;
+    E[levels + 1] = ceil_div<uint64_t>(E[levels], G);
+    ++levels;
+  }
+  // workspace: per level the elements (tails / aggregates) and their start states, the matrices,
+  // and a copy of the entry state (the history buffers are rewritten at the end)
+  size_t off[kMaxLevels + 1][2];
+  size_t bytes = 0;
+  for (int k = 0; k <= levels; ++k) {
+    off[k][0] = bytes;
+    bytes += E[k] * P * sizeof(A);
+    off[k][1] = bytes;
+    bytes += E[k] * P * sizeof(A);
+  }
+  const size_t off_m = bytes;
+  bytes += (size_t)(levels + 1) * kGroup * P * P * sizeof(double);  // T[level][r] = M_level^r
+  const size_t off_s0 = bytes;
+  bytes += P * sizeof(A);
+  const size_t off_st = bytes;  // exit state staged by the last chunk: P outputs, then P inputs
+  bytes += 2 * P * sizeof(A);
+  char* ws = nullptr;
+  hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&ws), bytes, st);
+  if (e != hipSuccess) return e;
+  auto elems = [&](int k) { return reinterpret_cast<A*>(ws + off[k][0]); };
+  auto starts = [&](int k) { return reinterpret_cast<A*>(ws + off[k][1]); };
+  auto table = [&](int k) { return reinterpret_cast<double*>(ws + off_m) + (size_t)k * kGroup * P * P; };
+  A* s0 = reinterpret_cast<A*>(ws + off_s0);
+  A* st_out = reinterpret_cast<A*>(ws + off_st);
+  const int K = cf.K;
+  const int Pk = K - 1;  // live state components (<= P); the rest stay zero
+
+  constexpr int WG = TileShape<S>::WG;
+  const uint32_t blocks = (uint32_t)ceil_div<uint64_t>(C, WG);
+  const SetupArgs sa{yh, s0, table(0), levels};
+  k_iir_chunks<S, P, kTails><<<blocks + 1, WG, 0, st>>>(cf, x, xh, n, nullptr, elems(0), nullptr, sa);
+  for (int k = 0; k <= levels; ++k) {  // the top level's aggregate is not needed
+    k_iir_up<A, P><<<(uint32_t)ceil_div<uint64_t>(E[k], kGroup), 64, 0, st>>>(elems(k), E[k], table(k), starts(k),
+                                                                           k < levels ? elems(k + 1) : nullptr);
+  }
+  for (int k = levels; k >= 0; --k) {
+    k_iir_down<A, P><<<(uint32_t)ceil_div<uint64_t>(E[k], kGroup), 64, 0, st>>>(
+        E[k], table(k), k < levels ? starts(k + 1) : nullptr, s0, starts(k));
+  }
+  k_iir_chunks<S, P, kFinal><<<blocks, WG, 0, st>>>(cf, x, xh, n, starts(0), st_out, y, SetupArgs{});
+  if (xh || yh) k_iir_history<S><<<1, 64, 0, st>>>(xh, yh, st_out, P, Pk);
+  e = launch_status();
+  const hipError_t f = hipFreeAsync(ws, st);
+  return e != hipSuccess ? e : f;
+}
+
+template <class S>
+static hipError_t entry(const float* b, const float* a, size_t K, S* xh, S* yh, const S* x, S* y, size_t n,
+                        int32_t device, hipStream_t st) {
+  if (K < 2 || K > 32) return hipErrorInvalidValue;  // reference limits (iir.cu:229-235)
+  if (n == 0) return hipSuccess;
+  if (b == nullptr || a == nullptr || x == nullptr || y == nullptr) return hipErrorInvalidValue;
+  static_assert(kChunk >= 31, "a chunk must hold the largest state");
+  DeviceScope scope(device);
+  if (scope.status() != hipSuccess) return scope.status();
+  const Coeffs cf{b, a, (int)K};
+  const size_t P = K - 1;
+  if (P <= 1) return run<S, 1>(cf, xh, yh, x, y, n, st);
+  if (P <= 2) return run<S, 2>(cf, xh, yh, x, y, n, st);
+  if (P <= 4) return run<S, 4>(cf, xh, yh, x, y, n, st);
+  if (P <= 8) return run<S, 8>(cf, xh, yh, x, y, n, st);
+  if (P <= 16) return run<S, 16>(cf, xh, yh, x, y, n, st);
+  return run<S, 31>(cf, xh, yh, x, y, n, st);
+}
+
+}  // namespace iir
+}  // namespace gsdr
+
+GSDR_C_LINKAGE hipError_t gsdrIirFF(const float* bCoeffs, const float* aCoeffs, size_t coeffCount, float* inputHistory,
+                                    float* outputHistory, const float* input, float* output, size_t numElements,
+                                    int32_t cudaDevice, hipStream_t cudaStream) GSDR_NO_EXCEPT {
+  return gsdr::iir::entry<float>(bCoeffs, aCoeffs, coeffCount, inputHistory, outputHistory, input, output,
+                                 numElements, cudaDevice, cudaStream);
+}
+
+GSDR_C_LINKAGE hipError_t gsdrIirCC(const float* bCoeffs, const float* aCoeffs, size_t coeffCount,
+                                    hipFloatComplex* inputHistory, hipFloatComplex* outputHistory,
+                                    const hipFloatComplex* input, hipFloatComplex* output, size_t numElements,
+                                    int32_t cudaDevice, hipStream_t cudaStream) GSDR_NO_EXCEPT {
+  return gsdr::iir::entry<float2>(bCoeffs, aCoeffs, coeffCount, reinterpret_cast<float2*>(inputHistory),
+                                  reinterpret_cast<float2*>(outputHistory), reinterpret_cast<const float2*>(input),
+                                  reinterpret_cast<float2*>(output), numElements, cudaDevice, cudaStream);
+}
+
+GSDR_C_LINKAGE hipError_t gsdrIirFFCustom(const float* bCoeffs, const float* aCoeffs, size_t coeffCount,
+                                          float* inputHistory, float* outputHistory, const float* input, float* output,
+                                          size_t numElements, size_t samplesPerThread, int32_t cudaDevice,
+                                          hipStream_t cudaStream) GSDR_NO_EXCEPT {
+  if (samplesPerThread == 0 || samplesPerThread > 32) return hipErrorInvalidValue;  // iir.cu (Custom) limits
+  return gsdrIirFF(bCoeffs, aCoeffs, coeffCount, inputHistory, outputHistory, input, output, numElements, cudaDevice,
+                   cudaStream);
+}
+
+GSDR_C_LINKAGE hipError_t gsdrIirCCCustom(const float* bCoeffs, const float* aCoeffs, size_t coeffCount,
+                                          hipFloatComplex* inputHistory, hipFloatComplex* outputHistory,
+                                          const hipFloatComplex* input, hipFloatComplex* output, size_t numElements,
+                                          size_t samplesPerThread, int32_t cudaDevice,
+                                          hipStream_t cudaStream) GSDR_NO_EXCEPT {
+  if (samplesPerThread == 0 || samplesPerThread > 32) return hipErrorInvalidValue;
+  return gsdrIirCC(bCoeffs, aCoeffs, coeffCount, inputHistory, outputHistory, input, output, numElements, cudaDevice,
+                   cudaStream);
+}

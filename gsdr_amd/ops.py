@@ -17,7 +17,7 @@ __all__ = [
     "qpsk_modulate_templated", "qpsk_demodulate_templated",
     "qpsk256_init", "qpsk256_modulate", "qpsk256_demodulate", "qpsk256_modulate_4x", "qpsk256_demodulate_4x",
     "nco_phase_increment", "stream_of",
-    "fm_demod_multi", "am_demod_multi", "add_const", "multiply", "add_to_magnitude", "abs_", "cosine", "int8_to_norm_float",
+    "fm_demod_multi", "am_demod_multi", "iir", "add_const", "multiply", "add_to_magnitude", "abs_", "cosine", "int8_to_norm_float",
 ]
 
 
@@ -216,6 +216,27 @@ def magnitude(x, out=None):
     out = torch.empty(n, dtype=torch.float32, device=x.device) if out is None else out
     _require(out, torch.float32, "output", n)
     check("gsdrMagnitude", lib.gsdrMagnitude(_ptr(x), _ptr(out), n, _dev(x), stream_of(x)))
+    return out
+
+
+def iir(b, a, x, x_hist=None, y_hist=None, out=None):
+    """gsdrIirFF / gsdrIirCC (iir.h): y[n] = sum b[i] x[n-i] - sum_{i>=1} a[i] y[n-i]. x_hist / y_hist
+    (K-1 samples, device tensors of x's dtype, or None) hold the state before x and are updated in
+    place with the state after it."""
+    _require(b, torch.float32, "bCoeffs")
+    _require(a, torch.float32, "aCoeffs", b.numel())
+    if x.dtype not in (torch.float32, torch.complex64):
+        raise TypeError(f"input: expected float32 or complex64, got {x.dtype}")
+    _require(x, x.dtype, "input")
+    K, n = b.numel(), x.numel()
+    for h, nm in ((x_hist, "inputHistory"), (y_hist, "outputHistory")):
+        if h is not None:
+            _require(h, x.dtype, nm, K - 1)
+    out = torch.empty_like(x) if out is None else out
+    _require(out, x.dtype, "output", n)
+    name = "gsdrIirCC" if x.dtype == torch.complex64 else "gsdrIirFF"
+    check(name, getattr(lib, name)(_ptr(b), _ptr(a), K, _ptr(x_hist), _ptr(y_hist), _ptr(x), _ptr(out), n,
+                                   _dev(x), stream_of(x)))
     return out
 
 

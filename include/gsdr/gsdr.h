@@ -11,6 +11,7 @@
 #include <gsdr/fm.h>
 #include <gsdr/gsdr_ext.h>
 #include <gsdr/hip_util.h>
+#include <gsdr/iir.h>
 #include <gsdr/qpsk.h>
 #include <gsdr/qpsk256.h>
 #include <gsdr/quad_demod.h>

@@ -371,3 +371,56 @@ void oracle_cosine(int complex_out, float phi_begin, float phi_end, float* out, 
     }
   }
 }
+
+/* ---------------------------------------------------------------- IIR (true recursion, in double) */
+
+void oracle_iir(int cplx, const float* b, const float* a, size_t K, float* xh, float* yh, const float* x, float* y,
+                size_t n) {
+  const size_t P = K - 1, W = cplx ? 2 : 1;
+  for (size_t w = 0; w < W; ++w) { /* real and imaginary recursions are independent */
+    double* xs = (double*)calloc(P + n, sizeof(double));
+    double* ys = (double*)calloc(P + n, sizeof(double));
+    /* index P + m holds sample m; P - 1 - i holds history entry i (sample -1-i) */
+    for (size_t i = 0; i < P; ++i) {
+      xs[P - 1 - i] = xh ? xh[i * W + w] : 0.0;
+      ys[P - 1 - i] = yh ? yh[i * W + w] : 0.0;
+    }
+    for (size_t m = 0; m < n; ++m) {
+      xs[P + m] = x[m * W + w];
+      double acc = 0.0;
+      for (size_t i = 0; i < K; ++i) acc += (double)b[i] * xs[P + m - i];
+      for (size_t i = 1; i < K; ++i) acc -= (double)a[i] * ys[P + m - i];
+      ys[P + m] = acc;
+      y[m * W + w] = (float)acc;
+    }
+    for (size_t i = 0; i < P; ++i) {
+      if (xh) xh[i * W + w] = (float)xs[P + n - 1 - i];
+      if (yh) yh[i * W + w] = (float)ys[P + n - 1 - i];
+    }
+    free(xs);
+    free(ys);
+  }
+}
+
+void oracle_iir_f32(int cplx, const float* b, const float* a, size_t K, const float* xh, const float* yh,
+                    const float* x, float* y, size_t n) {
+  const size_t P = K - 1, W = cplx ? 2 : 1;
+  for (size_t w = 0; w < W; ++w) {
+    float* xs = (float*)calloc(P + n, sizeof(float));
+    float* ys = (float*)calloc(P + n, sizeof(float));
+    for (size_t i = 0; i < P; ++i) {
+      xs[P - 1 - i] = xh ? xh[i * W + w] : 0.0f;
+      ys[P - 1 - i] = yh ? yh[i * W + w] : 0.0f;
+    }
+    for (size_t m = 0; m < n; ++m) {
+      xs[P + m] = x[m * W + w];
+      float acc = b[0] * xs[P + m];
+      for (size_t i = 1; i < K; ++i) acc = fmaf(b[i], xs[P + m - i], acc);
+      for (size_t i = 1; i < K; ++i) acc = fmaf(-a[i], ys[P + m - i], acc);
+      ys[P + m] = acc;
+      y[m * W + w] = acc;
+    }
+    free(xs);
+    free(ys);
+  }
+}

@@ -88,4 +88,17 @@ void oracle_abs(const float* x, float* out, size_t n);
 void oracle_int8_to_float(const int8_t* x, float* out, size_t n);
 void oracle_cosine(int complex_out, float phi_begin, float phi_end, float* out, size_t n);
 
+
+/* IIR (re-specified, include/gsdr/iir.h): y[n] = sum_{i<K} b[i] x[n-i] -
+ * sum_{1<=i<K} a[i] y[n-i], evaluated sequentially in double. xh / yh (K-1 entries, may be NULL) hold
+ * x[-1-i] / y[-1-i] on entry and the last K-1 inputs / outputs on return. cplx: samples are
+ * interleaved complex floats (two independent recursions). */
+void oracle_iir(int cplx, const float* b, const float* a, size_t K, float* xh, float* yh, const float* x, float* y,
+                size_t n);
+/* The same recursion as a plain sequential float32 loop (acc = b0 x; fmaf(b_i, x_{n-i}, acc);
+ * fmaf(-a_i, y_{n-i}, acc)): the error any sequential fp32 implementation makes, used to scale the
+ * GPU test bar to the filter's conditioning. */
+void oracle_iir_f32(int cplx, const float* b, const float* a, size_t K, const float* xh, const float* yh,
+                    const float* x, float* y, size_t n);
+
 #endif /* GSDR_ORACLE_H_ */

@@ -44,6 +44,8 @@ _SIG = {
     "oracle_abs": [_p, _p, _sz],
     "oracle_int8_to_float": [_p, _p, _sz],
     "oracle_cosine": [_int, _f, _f, _p, _sz],
+    "oracle_iir": [_int, _p, _p, _sz, _p, _p, _p, _p, _sz],
+    "oracle_iir_f32": [_int, _p, _p, _sz, _p, _p, _p, _p, _sz],
 }
 for _name, _args in _SIG.items():
     getattr(_lib, _name).argtypes = _args
@@ -254,3 +256,35 @@ def cosine(phi_begin, phi_end, n, complex_out=True):
     out = np.empty(n, np.complex64 if complex_out else np.float32)
     _lib.oracle_cosine(1 if complex_out else 0, float(phi_begin), float(phi_end), _ptr(out), n)
     return out
+
+
+def iir(b, a, x, x_hist=None, y_hist=None):
+    """IIR in double (include/gsdr/iir.h semantics). Returns (y, new_x_hist, new_y_hist); histories are
+    arrays of K-1 samples (x[-1-i], y[-1-i]) or None."""
+    b = _c(b, np.float32)
+    a = _c(a, np.float32)
+    K = b.size
+    cplx = np.iscomplexobj(x)
+    dt = np.complex64 if cplx else np.float32
+    x = _c(x, dt)
+    y = np.empty(x.size, dt)
+    xh = None if x_hist is None else _c(np.array(x_hist, dt).copy(), dt)
+    yh = None if y_hist is None else _c(np.array(y_hist, dt).copy(), dt)
+    _lib.oracle_iir(1 if cplx else 0, _ptr(b), _ptr(a), K, None if xh is None else _ptr(xh),
+                    None if yh is None else _ptr(yh), _ptr(x), _ptr(y), x.size)
+    return y, xh, yh
+
+
+def iir_f32(b, a, x, x_hist=None, y_hist=None):
+    """The IIR as a sequential float32 loop (error scale of any fp32 implementation)."""
+    b = _c(b, np.float32)
+    a = _c(a, np.float32)
+    cplx = np.iscomplexobj(x)
+    dt = np.complex64 if cplx else np.float32
+    x = _c(x, dt)
+    y = np.empty(x.size, dt)
+    xh = None if x_hist is None else _c(x_hist, dt)
+    yh = None if y_hist is None else _c(y_hist, dt)
+    _lib.oracle_iir_f32(1 if cplx else 0, _ptr(b), _ptr(a), b.size, None if xh is None else _ptr(xh),
+                        None if yh is None else _ptr(yh), _ptr(x), _ptr(y), x.size)
+    return y

@@ -398,10 +398,34 @@ __device__ __forceinline__ void store_fir(OutT* __restrict__ out, uint64_t k0, u
 
 // FM discriminator of consecutive FIR outputs: g * arg(y1 * conj(y0)) (reference src/fm.cu:66-68,
 // src/quad_demod.cu:30-31).
+// atan2 for the discriminators: octant reduction t = min/max (v_rcp_f32), an odd minimax polynomial
+// for atan on [0, 1] (max abs error 3.3e-7 rad in float32 evaluation, tools/atan_fit.py), then the
+// octant fix-ups. Zeros, infinities and NaN take the library atan2f, so its special values
+// (atan2(0, 0) = 0, atan2(+-0, -0) = +-pi, ...) are unchanged. The discriminator bar is 3.1e-5 rad
+// (1e-5 of pi; tests/helpers.py wrapped_angle_err).
+__device__ __forceinline__ float disc_atan2(float y, float x) {
+  const float ax = fabsf(x), ay = fabsf(y);
+  const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+  if (!(ax < INFINITY && ay < INFINITY) || mx == 0.0f) return atan2f(y, x);
+  const float t = mn * __builtin_amdgcn_rcpf(mx);
+  const float s = t * t;
+  float p = 0.006811787374317646f;
+  p = fmaf(p, s, -0.0336042121052742f);
+  p = fmaf(p, s, 0.07962368428707123f);
+  p = fmaf(p, s, -0.132333442568779f);
+  p = fmaf(p, s, 0.19807817041873932f);
+  p = fmaf(p, s, -0.3331736922264099f);
+  p = fmaf(p, s, 0.9999961256980896f);
+  float r = p * t;
+  if (ay > ax) r = 1.57079637f - r;
+  if (x < 0.0f) r = 3.14159274f - r;
+  return copysignf(r, y);
+}
+
 __device__ __forceinline__ float fm_disc(float2 y0, float2 y1, float g) {
   const float re = y1.x * y0.x + y1.y * y0.y;
   const float im = y1.y * y0.x - y1.x * y0.y;
-  return g * atan2f(im, re);
+  return g * disc_atan2(im, re);
 }
 
 // AM envelope: 2 * saturate(|y|) - 1, saturate(NaN) = 0 (reference src/am.cu:49, quad_demod.cu:47-48).

@@ -40,7 +40,7 @@ __device__ __forceinline__ float sqdist(float2 r, float2 c) {
   return __fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy));
 }
 
-__device__ __forceinline__ uint32_t demod_exhaustive(const float2* __restrict__ tab, float2 r) {
+__device__ __noinline__ uint32_t demod_exhaustive(const float2* __restrict__ tab, float2 r) {
   float best = INFINITY;
   uint32_t idx = 0;
   for (uint32_t i = 0; i < 256; ++i) {
@@ -60,28 +60,37 @@ __device__ __forceinline__ int nearest_level(float v, float scale) {
   return i < 0 ? 0 : (i > 15 ? 15 : i);
 }
 
-__device__ __forceinline__ uint32_t demod_rect(const float2* __restrict__ tab, float2 r, float a, float scale) {
-  const float lim = 4.0f * fabsf(a);
-  if (!(fabsf(r.x) <= lim && fabsf(r.y) <= lim) || !(scale == scale) || isinf(scale)) {
-    return demod_exhaustive(tab, r);
-  }
+// Rectangular fast path. Table entry 16 i + q is (lx[i], ly[q]) -- the I coordinate depends on i only
+// and the Q coordinate on q only (qpsk256.cu:33-34) -- so the 9 candidate distances are sums of 3 + 3
+// per-axis squares read from per-axis level arrays, bit-identical to sqdist() on the table entries.
+// Candidates are compared in ascending index order (i major, q minor) with strict '<'; a level
+// outside [0, 15] contributes +inf and never wins. Returns 256 when the symbol needs the exhaustive
+// search (outside |re|,|im| <= 4|a|, or NaN).
+__device__ __forceinline__ uint32_t demod_rect_fast(const float* __restrict__ lx, const float* __restrict__ ly, float2 r,
+                                                    float lim, float scale) {
+  if (!(fabsf(r.x) <= lim && fabsf(r.y) <= lim)) return 256u;
   const int i0 = nearest_level(r.x, scale);
   const int q0 = nearest_level(r.y, scale);
+  float ex[3], ey[3];
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    const int i = i0 - 1 + d, q = q0 - 1 + d;
+    const float cx = lx[i < 0 ? 0 : (i > 15 ? 15 : i)];
+    const float cy = ly[q < 0 ? 0 : (q > 15 ? 15 : q)];
+    const float dx = __fsub_rn(r.x, cx), dy = __fsub_rn(r.y, cy);
+    ex[d] = (i < 0 || i > 15) ? INFINITY : __fmul_rn(dx, dx);
+    ey[d] = (q < 0 || q > 15) ? INFINITY : __fmul_rn(dy, dy);
+  }
   float best = INFINITY;
   uint32_t idx = 0;
 #pragma unroll
-  for (int di = -1; di <= 1; ++di) {
-    const int i = i0 + di;
-    if (i < 0 || i > 15) continue;
+  for (int di = 0; di < 3; ++di) {
 #pragma unroll
-    for (int dq = -1; dq <= 1; ++dq) {
-      const int q = q0 + dq;
-      if (q < 0 || q > 15) continue;
-      const uint32_t k = (uint32_t)(i * 16 + q);
-      const float d = sqdist(r, tab[k]);
+    for (int dq = 0; dq < 3; ++dq) {
+      const float d = __fadd_rn(ex[di], ey[dq]);
       if (d < best) {
         best = d;
-        idx = k;
+        idx = (uint32_t)((i0 - 1 + di) * 16 + (q0 - 1 + dq));
       }
     }
   }
@@ -122,34 +131,43 @@ __global__ __launch_bounds__(kCBlock) void k_c256_mod(C256Streams st, uint32_t n
 
 __global__ __launch_bounds__(kCBlock) void k_c256_demod(C256Streams st, uint32_t n, uint32_t type) {
   __shared__ float2 tab[256];
-  load_table(tab, type);
+  __shared__ float lx[16], ly[16];
+  const float2* tsrc = c_qpsk256_tables[type == 0 ? 0 : 1];
+  for (uint32_t i = threadIdx.x; i < 256; i += kCBlock) tab[i] = tsrc[i];
+  if (threadIdx.x < 16) {
+    lx[threadIdx.x] = tsrc[threadIdx.x * 16].x;
+    ly[threadIdx.x] = tsrc[threadIdx.x].y;
+  }
+  __syncthreads();
   const float2* __restrict__ in = reinterpret_cast<const float2*>(st.in[blockIdx.y]);
   uint8_t* __restrict__ out = reinterpret_cast<uint8_t*>(st.out[blockIdx.y]);
   const uint64_t s0 = ((uint64_t)blockIdx.x * kCBlock + threadIdx.x) * kCSym;
   if (s0 >= n) return;
   const float a = tab[255].x;  // rectangular: (15 - 7.5) / 7.5 * a == a exactly
   const float scale = 7.5f / a;
-  const bool rect = (type == 0);
+  // the fast path needs a finite, non-zero amplitude (else every symbol takes the exhaustive search)
+  const float lim = (type == 0 && isfinite(scale)) ? 4.0f * fabsf(a) : -1.0f;
+  auto demod = [&](float2 r) -> uint32_t {
+    const uint32_t k = demod_rect_fast(lx, ly, r, lim, scale);
+    return k < 256u ? k : demod_exhaustive(tab, r);
+  };
   if (s0 + kCSym <= n && (reinterpret_cast<uintptr_t>(in + s0) & 15u) == 0 &&
       (reinterpret_cast<uintptr_t>(out + s0) & 15u) == 0) {
     const float4* src = reinterpret_cast<const float4*>(in + s0);
+    float4 v[kCSym / 2];
+#pragma unroll
+    for (int q = 0; q < kCSym / 2; ++q) v[q] = src[q];
     uint32_t words[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int q = 0; q < kCSym / 2; ++q) {
-      const float4 v = src[q];
-      const float2 r0 = make_float2(v.x, v.y);
-      const float2 r1 = make_float2(v.z, v.w);
-      const uint32_t i0 = rect ? demod_rect(tab, r0, a, scale) : demod_exhaustive(tab, r0);
-      const uint32_t i1 = rect ? demod_rect(tab, r1, a, scale) : demod_exhaustive(tab, r1);
+      const uint32_t i0 = demod(make_float2(v[q].x, v[q].y));
+      const uint32_t i1 = demod(make_float2(v[q].z, v[q].w));
       words[q / 2] |= (i0 | (i1 << 8)) << (16 * (q & 1));
     }
     *reinterpret_cast<uint4*>(out + s0) = make_uint4(words[0], words[1], words[2], words[3]);
   } else {
     for (int k = 0; k < kCSym; ++k) {
-      if (s0 + k < n) {
-        const float2 r = in[s0 + k];
-        out[s0 + k] = (uint8_t)(rect ? demod_rect(tab, r, a, scale) : demod_exhaustive(tab, r));
-      }
+      if (s0 + k < n) out[s0 + k] = (uint8_t)demod(in[s0 + k]);
     }
   }
 }

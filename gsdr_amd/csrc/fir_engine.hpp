@@ -299,6 +299,14 @@ __device__ __forceinline__ float4 stage_transform(float4 v, uint32_t s, const Fi
   return v;
 }
 
+// granules per staging batch: the largest divisor of the per-thread count that is at most 8
+constexpr int staging_batch(int bpt) {
+  for (int b = 8; b > 1; --b) {
+    if (bpt % b == 0) return b;
+  }
+  return 1;
+}
+
 // Stage granules [0, NG) of the tile starting at global sample S0 into LDS (padded layout).
 // The first SG*WG granules (the tile body) are loaded fully unrolled so every HBM load is in flight
 // before the first LDS write; the remaining halo granules follow in a short strided loop.
@@ -310,7 +318,7 @@ __device__ __forceinline__ void stage_tile(float4* __restrict__ lds, const InT* 
   constexpr int BPT = Geo::SG * (Geo::KT / Geo::ROUT) / WG;
   static_assert(BPT * WG == Geo::SG * (Geo::KT / Geo::ROUT), "tile body must split evenly over the threads");
   // at most 8 granules (128 B) in flight per lane: bounds the staging registers for large segments
-  constexpr int SB = BPT < 8 ? BPT : 8;
+  constexpr int SB = staging_batch(BPT);
   static_assert(BPT % SB == 0, "segment granules must split into whole staging batches");
   const uint32_t tid = threadIdx.x;
   // wave-uniform: is the whole staged span readable? (every tile but the last)

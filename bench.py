@@ -270,6 +270,20 @@ def secondary_configs(torch, ops, device, taps):
                       "modulate_us": round(tm * 1e6, 2), "demodulate_us": round(td * 1e6, 2),
                       "alg_gbps_mod": round(9 * n / tm / 1e9, 1), "alg_gbps_demod": round(9 * n / td / 1e9, 1),
                       "ser": round(float((rx_bytes != syms).float().mean()), 6)}
+    # circular table (per-cell candidate lists), same symbols, sigma 0.01/axis
+    ops.qpsk256_init(1, 1.0, device.index)
+    ops.qpsk256_modulate(syms, 1, out=tx)
+    rx = tx + torch.randn(n, dtype=torch.complex64, device=device, generator=g) * (0.01 * np.sqrt(2.0))
+    ops.qpsk256_demodulate(rx, 1, out=rx_bytes)
+    s3, e3 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s3.record()
+    for _ in range(reps):
+        ops.qpsk256_demodulate(rx, 1, out=rx_bytes)
+    e3.record()
+    torch.cuda.synchronize()
+    tc = s3.elapsed_time(e3) / reps * 1e-3
+    out["qpsk256"]["demodulate_circular_us"] = round(tc * 1e6, 2)
+    out["qpsk256"]["ser_circular_sigma_0.01"] = round(float((rx_bytes != syms).float().mean()), 6)
     return out
 
 

@@ -18,6 +18,9 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+#include <algorithm>
+#include <cmath>
+
 #include "gsdr/qpsk256.h"
 #include "launch.hpp"
 
@@ -28,6 +31,22 @@ constexpr int kCSym = 16;  // symbols per thread
 
 // [0] rectangular, [1] circular; per device (module globals are per-device copies).
 __constant__ float2 c_qpsk256_tables[2][256];
+
+// Circular table: per-cell candidate lists over a kCellGrid^2 grid covering [-R, R)^2, built on the
+// host by gsdrQpsk256InitConstellation. List of cell c = idx[start[c] .. start[c+1]), ascending.
+// A point is listed for a cell when its distance to the cell is at most the smallest worst-case
+// distance of any table point over the cell (plus a margin for float rounding), so every point that
+// can win the argmin anywhere in the cell -- ties included -- is on the list, and the argmin over the
+// list in index order with the same sqdist() is the exhaustive one. R == 0 disables the lookup.
+constexpr int kCellGrid = 48;
+constexpr int kMaxCellEntries = 8192;
+struct CircCells {
+  float R;
+  float inv_cs;  // kCellGrid / (2 R)
+  uint16_t start[kCellGrid * kCellGrid + 1];
+  alignas(4) uint8_t idx[kMaxCellEntries];
+};
+__device__ CircCells g_circ_cells;
 
 struct C256Streams {
   const void* in[4];
@@ -132,11 +151,19 @@ __global__ __launch_bounds__(kCBlock) void k_c256_mod(C256Streams st, uint32_t n
 __global__ __launch_bounds__(kCBlock) void k_c256_demod(C256Streams st, uint32_t n, uint32_t type) {
   __shared__ float2 tab[256];
   __shared__ float lx[16], ly[16];
+  __shared__ uint16_t cstart[kCellGrid * kCellGrid + 1];
+  __shared__ uint8_t cidx[kMaxCellEntries];
   const float2* tsrc = c_qpsk256_tables[type == 0 ? 0 : 1];
   for (uint32_t i = threadIdx.x; i < 256; i += kCBlock) tab[i] = tsrc[i];
   if (threadIdx.x < 16) {
     lx[threadIdx.x] = tsrc[threadIdx.x * 16].x;
     ly[threadIdx.x] = tsrc[threadIdx.x].y;
+  }
+  if (type != 0 && g_circ_cells.R > 0.0f) {  // the circular candidate lists, into LDS
+    for (uint32_t i = threadIdx.x; i <= (uint32_t)(kCellGrid * kCellGrid); i += kCBlock) cstart[i] = g_circ_cells.start[i];
+    const uint32_t total = g_circ_cells.start[kCellGrid * kCellGrid];
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(g_circ_cells.idx);
+    for (uint32_t i = threadIdx.x; i < (total + 3) / 4; i += kCBlock) reinterpret_cast<uint32_t*>(cidx)[i] = src[i];
   }
   __syncthreads();
   const float2* __restrict__ in = reinterpret_cast<const float2*>(st.in[blockIdx.y]);
@@ -145,11 +172,32 @@ __global__ __launch_bounds__(kCBlock) void k_c256_demod(C256Streams st, uint32_t
   if (s0 >= n) return;
   const float a = tab[255].x;  // rectangular: (15 - 7.5) / 7.5 * a == a exactly
   const float scale = 7.5f / a;
-  // the fast path needs a finite, non-zero amplitude (else every symbol takes the exhaustive search)
+  // the fast paths need a finite, non-zero amplitude (else every symbol takes the exhaustive search)
   const float lim = (type == 0 && isfinite(scale)) ? 4.0f * fabsf(a) : -1.0f;
+  const float cR = type == 0 ? 0.0f : g_circ_cells.R;
+  const float inv_cs = g_circ_cells.inv_cs;
   auto demod = [&](float2 r) -> uint32_t {
-    const uint32_t k = demod_rect_fast(lx, ly, r, lim, scale);
-    return k < 256u ? k : demod_exhaustive(tab, r);
+    if (type == 0) {
+      const uint32_t k = demod_rect_fast(lx, ly, r, lim, scale);
+      return k < 256u ? k : demod_exhaustive(tab, r);
+    }
+    const float fx = (r.x + cR) * inv_cs, fy = (r.y + cR) * inv_cs;
+    if (cR > 0.0f && fx >= 0.0f && fy >= 0.0f && fx < (float)kCellGrid && fy < (float)kCellGrid) {
+      const int c = (int)fy * kCellGrid + (int)fx;
+      const uint32_t b = cstart[c], e = cstart[c + 1];
+      float best = INFINITY;
+      uint32_t idx = 0;
+      for (uint32_t m = b; m < e; ++m) {
+        const uint32_t k = cidx[m];
+        const float d = sqdist(r, tab[k]);
+        if (d < best) {  // ascending list: first index wins ties, as the exhaustive search
+          best = d;
+          idx = k;
+        }
+      }
+      return idx;
+    }
+    return demod_exhaustive(tab, r);
   };
   if (s0 + kCSym <= n && (reinterpret_cast<uintptr_t>(in + s0) & 15u) == 0 &&
       (reinterpret_cast<uintptr_t>(out + s0) & 15u) == 0) {
@@ -223,6 +271,47 @@ static void build_table(uint32_t type, float amplitude, float2* t) {
   }
 }
 
+// Candidate lists for the circular table (see CircCells). Distances in double on the float table.
+static bool build_cells(const float2* t, CircCells* cc) {
+  double rmax = 0.0;
+  for (int i = 0; i < 256; ++i) rmax = std::max(rmax, std::hypot((double)t[i].x, (double)t[i].y));
+  cc->R = 0.0f;
+  if (!(rmax > 0.0) || !std::isfinite(rmax)) return true;  // degenerate table: exhaustive search
+  const float R = (float)(rmax * 1.02);
+  const float inv_cs = (float)kCellGrid / (2.0f * R);
+  const double cs = 1.0 / (double)inv_cs;
+  const double margin = 1e-4 * rmax;  // >> float rounding of positions and distances
+  int n = 0;
+  for (int iy = 0; iy < kCellGrid; ++iy) {
+    for (int ix = 0; ix < kCellGrid; ++ix) {
+      const double x0 = -(double)R + ix * cs, x1 = x0 + cs, y0 = -(double)R + iy * cs, y1 = y0 + cs;
+      double bound = INFINITY;
+      for (int q = 0; q < 256; ++q) {
+        const double dx = std::max(std::fabs(t[q].x - x0), std::fabs(t[q].x - x1));
+        const double dy = std::max(std::fabs(t[q].y - y0), std::fabs(t[q].y - y1));
+        bound = std::min(bound, std::hypot(dx, dy));
+      }
+      bound += margin;
+      cc->start[iy * kCellGrid + ix] = (uint16_t)n;
+      for (int p = 0; p < 256; ++p) {
+        const double dx = std::max({x0 - t[p].x, 0.0, t[p].x - x1});
+        const double dy = std::max({y0 - t[p].y, 0.0, t[p].y - y1});
+        if (std::hypot(dx, dy) <= bound) {
+          if (n >= kMaxCellEntries) {
+            cc->R = 0.0f;
+            return true;  // does not fit: keep the exhaustive search
+          }
+          cc->idx[n++] = (uint8_t)p;
+        }
+      }
+    }
+  }
+  cc->start[kCellGrid * kCellGrid] = (uint16_t)n;
+  cc->R = R;
+  cc->inv_cs = inv_cs;
+  return true;
+}
+
 }  // namespace gsdr
 
 using gsdr::C256Streams;
@@ -237,6 +326,13 @@ GSDR_C_LINKAGE hipError_t gsdrQpsk256InitConstellation(uint32_t constellationTyp
   hipError_t st = hipMemcpyToSymbolAsync(HIP_SYMBOL(gsdr::c_qpsk256_tables), table, sizeof(table), offset,
                                          hipMemcpyHostToDevice, cudaStream);
   if (st != hipSuccess) return st;
+  static thread_local gsdr::CircCells cells;  // host staging (8 KiB+): waited for below
+  if (constellationType != 0) {
+    gsdr::build_cells(table, &cells);
+    st = hipMemcpyToSymbolAsync(HIP_SYMBOL(gsdr::g_circ_cells), &cells, sizeof(cells), 0, hipMemcpyHostToDevice,
+                                cudaStream);
+    if (st != hipSuccess) return st;
+  }
   // the host table lives on this stack frame: wait for the copy before returning
   return hipStreamSynchronize(cudaStream);
 }

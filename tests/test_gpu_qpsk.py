@@ -182,3 +182,19 @@ def test_qpsk256_config5_round_trip(cuda):
     for k0 in (0, n // 2, n - (1 << 18)):
         k1 = k0 + (1 << 18)
         assert np.array_equal(got_np[k0:k1], o.qpsk256_demod(table, rx_np[k0:k1]))
+
+
+@pytest.mark.parametrize("amp", [1.0, 0.37, -2.5])
+def test_qpsk256_circular_cells_bit_exact_dense(cuda, amp):
+    """The circular table's per-cell candidate lists (qpsk256.hip CircCells) reproduce the exhaustive
+    argmin bit for bit: 4 M points uniform over a square larger than the grid (outside -> exhaustive)."""
+    from gsdr_amd import ops
+
+    ops.qpsk256_init(1, amp)
+    table = o.qpsk256_table(1, amp)
+    rng = np.random.default_rng(int(abs(amp) * 100))
+    n = 1 << 22
+    span = 2.2 * abs(amp)
+    rx = (rng.uniform(-span, span, n) + 1j * rng.uniform(-span, span, n)).astype(np.complex64)
+    got = ops.qpsk256_demodulate(dev(rx, cuda), 1).cpu().numpy()
+    assert np.array_equal(got, o.qpsk256_demod(table, rx))

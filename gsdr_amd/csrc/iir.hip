@@ -280,16 +280,14 @@ __global__ __launch_bounds__(TileShape<S>::WG) void k_iir_chunks(Coeffs cf, cons
   }
 }
 
-// Up-sweep of one level: wave g scans its 64 elements (lane r = element j0 + r) from zero state,
-// Hillis-Steele over the affine composition: v_r <- v_r + M^(2^s) v_(r-2^s). Lane r's result is the
-// zero-state prefix through element r (kept in `incl` for the down-sweep); lane 63's is the group
-// aggregate for the next level.
+// Up-sweep of group g of one level (one wave, lane r = element g*64 + r): Hillis-Steele over the
+// affine composition from zero state, v_r <- v_r + M^(2^s) v_(r-2^s). Lane r's result is the
+// zero-state prefix through element r (kept in `incl` for the down-sweep); the group's last lane holds
+// the group aggregate for the next level.
 template <class A, int P>
-__global__ __launch_bounds__(64) void k_iir_up(const A* __restrict__ elems, uint64_t E, const double* __restrict__ T,
-                                               A* __restrict__ incl, A* __restrict__ aggs) {
+__device__ __forceinline__ void up_group(const A* __restrict__ elems, uint64_t E, const double* __restrict__ T,
+                                         A* __restrict__ incl, A* __restrict__ aggs, uint64_t g, int r) {
   constexpr int PP = P * P;
-  const uint64_t g = blockIdx.x;
-  const int r = threadIdx.x;
   const uint64_t j = g * kGroup + r;
   const uint64_t last = (E - 1 < g * kGroup + kGroup - 1) ? E - 1 - g * kGroup : kGroup - 1;
   A v[P];
@@ -322,16 +320,13 @@ __global__ __launch_bounds__(64) void k_iir_up(const A* __restrict__ elems, uint
   }
 }
 
-// Down-sweep of one level: element j = g*64 + r starts in state M^r S_g + prefix_(r-1), with S_g the
+// Down-sweep of group g: element j = g*64 + r starts in state M^r S_g + prefix_(r-1), with S_g the
 // group's start state (group_starts[g], or s0 at the top level) and prefix the up-sweep's inclusive
 // zero-state prefix of the previous lane. Overwrites incl with the start states.
 template <class A, int P>
-__global__ __launch_bounds__(64) void k_iir_down(uint64_t E, const double* __restrict__ T,
-                                                 const A* __restrict__ group_starts, const A* __restrict__ s0,
-                                                 A* __restrict__ incl_starts) {
+__device__ __forceinline__ void down_group(uint64_t E, const double* __restrict__ T, const A* __restrict__ group_starts,
+                                           const A* __restrict__ s0, A* __restrict__ incl_starts, uint64_t g, int r) {
   constexpr int PP = P * P;
-  const uint64_t g = blockIdx.x;
-  const int r = threadIdx.x;
   const uint64_t j = g * kGroup + r;
   A pre[P], sg[P];
 #pragma unroll
@@ -340,14 +335,65 @@ __global__ __launch_bounds__(64) void k_iir_down(uint64_t E, const double* __res
     pre[i] = shfl_up_s(mine, 1);
     sg[i] = group_starts ? group_starts[g * P + i] : s0[i];
   }
-  if (j >= E) return;
-  const double* __restrict__ Mr = T + (size_t)r * PP;
+  if (j < E) {
+    const double* __restrict__ Mr = T + (size_t)r * PP;
 #pragma unroll
-  for (int i = 0; i < P; ++i) {
-    A acc = r > 0 ? pre[i] : zero_s(A{});
+    for (int i = 0; i < P; ++i) {
+      A acc = r > 0 ? pre[i] : zero_s(A{});
 #pragma unroll
-    for (int l = 0; l < P; ++l) acc = fma_s(Mr[i * P + l], sg[l], acc);
-    incl_starts[j * P + i] = acc;
+      for (int l = 0; l < P; ++l) acc = fma_s(Mr[i * P + l], sg[l], acc);
+      incl_starts[j * P + i] = acc;
+    }
+  }
+}
+
+// level 0 (many groups): one wave per group
+template <class A, int P>
+__global__ __launch_bounds__(64) void k_iir_up(const A* __restrict__ elems, uint64_t E, const double* __restrict__ T,
+                                               A* __restrict__ incl, A* __restrict__ aggs) {
+  up_group<A, P>(elems, E, T, incl, aggs, blockIdx.x, threadIdx.x);
+}
+
+template <class A, int P>
+__global__ __launch_bounds__(64) void k_iir_down(uint64_t E, const double* __restrict__ T,
+                                                 const A* __restrict__ group_starts, A* __restrict__ incl_starts) {
+  down_group<A, P>(E, T, group_starts, nullptr, incl_starts, blockIdx.x, threadIdx.x);
+}
+
+// The upper levels with at most kRestWaves groups run in one workgroup (one wave per group, a barrier
+// between levels, workgroup-scope visibility); larger levels get one launch each (a single workgroup
+// walking many groups serially is latency-bound).
+constexpr int kRestWaves = 16;
+template <class A>
+struct Levels {
+  A* elems[kMaxLevels + 1];
+  A* starts[kMaxLevels + 1];
+  const double* T[kMaxLevels + 1];
+  uint64_t E[kMaxLevels + 1];
+  int levels;
+};
+
+template <class A, int P>
+__global__ __launch_bounds__(64 * kRestWaves) void k_iir_up_rest(Levels<A> L, int first) {
+  const int w = threadIdx.x / 64, r = threadIdx.x % 64;
+  for (int k = first; k <= L.levels; ++k) {
+    const uint64_t groups = ceil_div<uint64_t>(L.E[k], kGroup);
+    for (uint64_t g = w; g < groups; g += kRestWaves) {
+      up_group<A, P>(L.elems[k], L.E[k], L.T[k], L.starts[k], k < L.levels ? L.elems[k + 1] : nullptr, g, r);
+    }
+    __syncthreads();
+  }
+}
+
+template <class A, int P>
+__global__ __launch_bounds__(64 * kRestWaves) void k_iir_down_rest(Levels<A> L, const A* __restrict__ s0, int lowest) {
+  const int w = threadIdx.x / 64, r = threadIdx.x % 64;
+  for (int k = L.levels; k >= lowest; --k) {
+    const uint64_t groups = ceil_div<uint64_t>(L.E[k], kGroup);
+    for (uint64_t g = w; g < groups; g += kRestWaves) {
+      down_group<A, P>(L.E[k], L.T[k], k < L.levels ? L.starts[k + 1] : nullptr, s0, L.starts[k], g, r);
+    }
+    __syncthreads();
   }
 }
 
@@ -407,13 +453,26 @@ static hipError_t run(const Coeffs& cf, S* xh, S* yh, const S* x, S* y, uint64_t
   const uint32_t blocks = (uint32_t)ceil_div<uint64_t>(C, WG);
   const SetupArgs sa{yh, s0, table(0), levels};
   k_iir_chunks<S, P, kTails><<<blocks + 1, WG, 0, st>>>(cf, x, xh, n, nullptr, elems(0), nullptr, sa);
-  for (int k = 0; k <= levels; ++k) {  // the top level's aggregate is not needed
-    k_iir_up<A, P><<<(uint32_t)ceil_div<uint64_t>(E[k], kGroup), 64, 0, st>>>(elems(k), E[k], table(k), starts(k),
-                                                                           k < levels ? elems(k + 1) : nullptr);
+  // levels with more than kRestWaves groups: one launch each; the rest: one single-workgroup launch
+  Levels<A> L{};
+  for (int k = 0; k <= levels; ++k) {
+    L.elems[k] = elems(k);
+    L.starts[k] = starts(k);
+    L.T[k] = table(k);
+    L.E[k] = E[k];
   }
-  for (int k = levels; k >= 0; --k) {
-    k_iir_down<A, P><<<(uint32_t)ceil_div<uint64_t>(E[k], kGroup), 64, 0, st>>>(
-        E[k], table(k), k < levels ? starts(k + 1) : nullptr, s0, starts(k));
+  L.levels = levels;
+  int rest = 0;  // first level handled by the single-workgroup kernels
+  while (rest <= levels && ceil_div<uint64_t>(E[rest], kGroup) > (uint64_t)kRestWaves) ++rest;
+  for (int k = 0; k < rest; ++k) {
+    k_iir_up<A, P><<<(uint32_t)ceil_div<uint64_t>(E[k], kGroup), 64, 0, st>>>(elems(k), E[k], table(k), starts(k),
+                                                                             elems(k + 1));
+  }
+  k_iir_up_rest<A, P><<<1, 64 * kRestWaves, 0, st>>>(L, rest);
+  k_iir_down_rest<A, P><<<1, 64 * kRestWaves, 0, st>>>(L, s0, rest);
+  for (int k = rest - 1; k >= 0; --k) {
+    k_iir_down<A, P><<<(uint32_t)ceil_div<uint64_t>(E[k], kGroup), 64, 0, st>>>(E[k], table(k), starts(k + 1),
+                                                                               starts(k));
   }
   k_iir_chunks<S, P, kFinal><<<blocks, WG, 0, st>>>(cf, x, xh, n, starts(0), st_out, y, SetupArgs{});
   if (xh || yh) k_iir_history<S><<<1, 64, 0, st>>>(xh, yh, st_out, P, Pk);

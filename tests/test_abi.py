@@ -100,6 +100,50 @@ def test_host_argument_validation_without_device_work(abi):
         HIP_ERROR_INVALID_VALUE
 
 
+def test_extension_validation_without_device_work(abi):
+    """The gsdrx extensions and the IIR / element-wise entry points reject bad arguments (or accept
+    empty work) before touching a device, as the core entry points do."""
+    lib = abi.lib
+    null = None
+    dummy = ctypes.c_void_p(16)
+    # int8 front end
+    assert lib.gsdrxFirFCInt8(4, null, 127, null, null, 0, 0, null) == HIP_SUCCESS
+    assert lib.gsdrxFirFCInt8(0, dummy, 127, dummy, dummy, 16, 0, null) == HIP_ERROR_INVALID_VALUE
+    assert lib.gsdrxFmDemodInt8(1e6, 0.0, 1e5, 2e4, 0, 0, dummy, 127, dummy, dummy, 16, 0, null) == \
+        HIP_ERROR_INVALID_VALUE
+    # multi-channel: no channels / no outputs succeed; missing channel arrays or bad format fail
+    assert lib.gsdrxFmDemodMulti(1e6, 0.0, null, null, 0, 4, 0, dummy, 127, 0, dummy, dummy, 16, 0, null) == \
+        HIP_SUCCESS
+    assert lib.gsdrxFmDemodMulti(1e6, 0.0, null, null, 3, 4, 0, dummy, 127, 0, dummy, dummy, 16, 0, null) == \
+        HIP_ERROR_INVALID_VALUE
+    chans = (ctypes.c_float * 2)(1e5, 2e5)
+    assert lib.gsdrxAmDemodMulti(1e6, 0.0, chans, 2, 4, 0, dummy, 127, 7, dummy, dummy, 16, 0, null) == \
+        HIP_ERROR_INVALID_VALUE
+    # IIR: the reference's coefficient-count limits, empty input, Custom samplesPerThread limits
+    for K in (0, 1, 33):
+        assert lib.gsdrIirFF(dummy, dummy, K, null, null, dummy, dummy, 16, 0, null) == HIP_ERROR_INVALID_VALUE
+    assert lib.gsdrIirCC(dummy, dummy, 5, null, null, null, null, 0, 0, null) == HIP_SUCCESS
+    assert lib.gsdrIirFFCustom(dummy, dummy, 5, null, null, dummy, dummy, 16, 0, 0, null) == HIP_ERROR_INVALID_VALUE
+    assert lib.gsdrIirCCCustom(dummy, dummy, 5, null, null, dummy, dummy, 16, 33, 0, null) == HIP_ERROR_INVALID_VALUE
+    # element-wise: empty work succeeds, missing operands fail
+    assert lib.gsdrMultiplyCC(null, null, null, 0, 0, null) == HIP_SUCCESS
+    assert lib.gsdrMultiplyFF(dummy, null, dummy, 16, 0, null) == HIP_ERROR_INVALID_VALUE
+    assert lib.gsdrCosineC(0.0, 1.0, null, 0, 0, null) == HIP_SUCCESS
+    assert lib.gsdrInt8ToNormFloat(null, dummy, 16, 0, null) == HIP_ERROR_INVALID_VALUE
+    # streaming object: creation argument checks, null handle, zero-length process
+    h = ctypes.c_void_p()
+    assert lib.gsdrxStreamCreate(null, 0, 0, 4, dummy, 127, 1.0, 0.0, 0.0, 1.0, 0, 0) == HIP_ERROR_INVALID_VALUE
+    assert lib.gsdrxStreamCreate(ctypes.byref(h), 0, 0, 0, dummy, 127, 1.0, 0.0, 0.0, 1.0, 0, 0) == \
+        HIP_ERROR_INVALID_VALUE
+    assert lib.gsdrxStreamCreate(ctypes.byref(h), 3, 0, 4, dummy, 127, 1.0, 0.0, 0.0, 1.0, 0, 0) == \
+        HIP_ERROR_INVALID_VALUE
+    assert lib.gsdrxStreamCreate(ctypes.byref(h), 0, 2, 4, dummy, 127, 1.0, 0.0, 0.0, 1.0, 0, 0) == \
+        HIP_ERROR_INVALID_VALUE
+    assert lib.gsdrxStreamProcess(null, dummy, 16, dummy, 16, null, null) == HIP_ERROR_INVALID_VALUE
+    assert lib.gsdrxStreamOutputsFor(null, 100) == 0
+    assert lib.gsdrxStreamDestroy(null) == HIP_SUCCESS
+
+
 def test_ops_module_imports(abi):
     from gsdr_amd import ops
 

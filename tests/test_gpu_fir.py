@@ -180,3 +180,15 @@ def test_fir_linearity(cuda):
     rhs = a * ops.fir(t, dev(x1, cuda), D, N) + b * ops.fir(t, dev(x2, cuda), D, N)
     s = bound(taps, np.abs(a * x1) + np.abs(b * x2), D, N)
     assert normwise_err(lhs.cpu().numpy(), rhs.cpu().numpy(), s) <= 2 * FLOAT_TOL
+
+
+@pytest.mark.parametrize("tt", ["FC", "FF", "CC", "CF"])
+@pytest.mark.parametrize("D,T", [(4, 1001), (4, 4001), (4, 6000), (2, 2500), (8, 3001), (1, 2048)])
+def test_fir_long_filters(cuda, tt, D, T):
+    """Long filters: the polyphase tile grows with the tap span until it leaves the 64 KB LDS budget
+    (near T = 4000 at D = 4), after which the generic kernel runs; both sides of that boundary."""
+    N = 3000 + D
+    taps, x = make(tt, T, (N - 1) * D + T, T + D)
+    y = run_fir(cuda, taps, x, D, N)
+    ref = o.fir(taps, x, D, N)
+    assert normwise_err(y, ref, bound(taps, x, D, N)) <= FLOAT_TOL

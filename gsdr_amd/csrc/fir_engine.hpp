@@ -19,7 +19,11 @@
 //   * A thread's segment is SG granules; when SG is even a one-granule pad is inserted after each
 //     segment so the per-lane stride is odd and the 16-lane groups of ds_read_b128 are bank-conflict
 //     free, while every window offset stays a compile-time constant.
-//   * No MFMA: 12.7 flop/byte at T=127, D=4 is an HBM-bound 1-D correlation.
+//   * Input may also be interleaved int8 I/Q (Iq8): converted to float as it is staged, so the float
+//     samples exist only in LDS. HBM loads and FIR stores are non-temporal (streamed once).
+//   * No MFMA: at T=127, D=4 (12.7 flop/byte) FP32 MFMA is no faster than packed VALU on gfx950 and a
+//     Toeplitz GEMM form adds ~47 % FLOPs; bf16-split MFMA costs as much energy as it saves. The kernel
+//     is bound by the part's 1400 W power cap with staging and MACs together.
 #pragma once
 
 #include <hip/hip_runtime.h>

@@ -61,7 +61,7 @@ hipError_t launch_generic(const FirJob& j, hipStream_t s) {
   return launch_status();
 }
 
-template <class TapT, class InT, int D, int R, int JC, int WG, int MODE, int ABL = 0, bool NT = false>
+template <class TapT, class InT, int D, int R, int JC, int WG, int MODE, int ABL = 0, bool NT = false, bool XM = false>
 hipError_t launch_poly(const FirJob& j, hipStream_t s) {
   using Geo = TileGeo<InT, D, R, WG>;
   FirParams p = make_params(j);
@@ -79,9 +79,9 @@ hipError_t launch_poly(const FirJob& j, hipStream_t s) {
   constexpr uint64_t A = SampleT<InT>::kSrcAlign;
   const bool vec = (reinterpret_cast<uintptr_t>(j.in) % A) == 0 && ((uint64_t)stride * D * sizeof(InT)) % A == 0;
   if (vec) {
-    k_fir_poly<TapT, InT, D, R, JC, WG, true, MODE, ABL, NT><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
+    k_fir_poly<TapT, InT, D, R, JC, WG, true, MODE, ABL, NT, XM><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
   } else {
-    k_fir_poly<TapT, InT, D, R, JC, WG, false, MODE, ABL, NT><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
+    k_fir_poly<TapT, InT, D, R, JC, WG, false, MODE, ABL, NT, XM><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
   }
   return launch_status();
 }
@@ -112,7 +112,8 @@ hipError_t launch_contig(const FirJob& j, hipStream_t s) {
 // Tile-shape variants of the headline case (real taps, complex input, D = 4), selectable through
 // gsdrxFirFCVariant for tuning sweeps (all with non-temporal streaming unless noted):
 //   0 default WG=256 R=4 JC=16 | 1 WG=128 R=8 | 3 WG=64 R=8 | 4 WG=128 R=8 JC=32 | 5 WG=256 R=4 JC=8
-//   7 generic kernel | 8 default shape with plain (temporal) loads/stores | 24 WG=64 R=4 | 28 WG=128 R=4
+//   7 generic kernel | 8 default shape with plain (temporal) loads/stores | 9 default, XCD-aware tile order
+//   24 WG=64 R=4 | 28 WG=128 R=4
 // Ablation probes (fir.hip): 104 compute only, 105 staging only, 107 staging only (non-temporal),
 // 110/111 streaming ceiling of this traffic mix (plain / non-temporal).
 hipError_t launch_fc_probe(const FirJob& j, hipStream_t s);
@@ -135,6 +136,8 @@ hipError_t launch_d4_complex(const FirJob& j, hipStream_t s) {
       return launch_generic<TapT, InT, MODE>(j, s);
     case 8:
       return launch_poly<TapT, InT, 4, 4, 16, 256, MODE>(j, s);
+    case 9:  // default shape, XCD-aware tile order
+      return launch_poly<TapT, InT, 4, 4, 16, 256, MODE, 0, true, true>(j, s);
     case 24:
       return launch_poly<TapT, InT, 4, 4, 16, 64, MODE, 0, true>(j, s);
     case 28:

@@ -526,7 +526,23 @@ __device__ __forceinline__ void poly_compute(const float4* __restrict__ lds, con
 // ABL (ablation, tuning probes only): 0 = full kernel, 1 = staging only, 2 = compute only.
 // NT: non-temporal (streaming) HBM loads for the staged input.
 // ------------------------------------------------------------------------------------------------
-template <class TapT, class InT, int D, int R, int JC, int WG, bool VEC, int MODE, int ABL = 0, bool NT = false>
+// Tile of workgroup b. XCD-aware (XM): workgroups are dispatched round-robin over the 8 XCDs, so
+// with the identity map neighbouring tiles (which share a halo of input rows) sit on different L2s;
+// remapped, XCD x walks one contiguous range of tiles and the halo of the previous tile is still in
+// its L2.
+template <bool XM>
+__device__ __forceinline__ uint32_t tile_of_block() {
+  if constexpr (!XM) {
+    return blockIdx.x;
+  } else {
+    const uint32_t nb = gridDim.x, b = blockIdx.x;
+    const uint32_t per = nb / 8, rem = nb % 8, x = b % 8, i = b / 8;
+    return x * per + (x < rem ? x : rem) + i;
+  }
+}
+
+template <class TapT, class InT, int D, int R, int JC, int WG, bool VEC, int MODE, int ABL = 0, bool NT = false,
+          bool XM = false>
 __global__ __launch_bounds__(WG) void k_fir_poly(FirParams p) {
   using Geo = TileGeo<InT, D, R, WG>;
   using OutT = typename Product<TapT, InT>::type;
@@ -535,7 +551,7 @@ __global__ __launch_bounds__(WG) void k_fir_poly(FirParams p) {
   extern __shared__ __attribute__((aligned(16))) float4 lds[];
   const InT* __restrict__ in = reinterpret_cast<const InT*>(p.in);
 
-  const uint64_t out0 = (uint64_t)blockIdx.x * p.tile_stride;
+  const uint64_t out0 = (uint64_t)tile_of_block<XM>() * p.tile_stride;
   const uint64_t S0 = out0 * D;
   const uint32_t span = p.nch * JC * D;
   const uint32_t NG = ((Geo::KT - 1) * D + span + G - 1) / G;

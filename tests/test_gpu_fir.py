@@ -110,7 +110,7 @@ def test_fir_restores_current_device(cuda):
     assert torch.cuda.current_device() == 0
 
 
-@pytest.mark.parametrize("variant", [0, 1, 3, 4, 5, 7, 8, 24, 28])
+@pytest.mark.parametrize("variant", [0, 1, 3, 4, 5, 7, 8, 9, 24, 28])
 def test_fir_fc_d4_variants(cuda, variant):
     """Every tile shape of the headline kernel (gsdrxFirFCVariant) meets the same bar."""
     from gsdr_amd import ops

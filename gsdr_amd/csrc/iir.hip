@@ -186,8 +186,10 @@ __device__ void iir_setup(const Coeffs& cf, const S* __restrict__ yh, typename A
 // (chunk stride kChunk + 1 elements: consecutive lanes land on different banks).
 template <class S>
 struct TileShape {
-  static constexpr int WG = sizeof(S) == 4 ? 256 : 128;  // 33 KB of LDS either way
-  static constexpr int TS = WG * kChunk;
+  static constexpr int WG = 256;
+  static constexpr int NC = sizeof(S) / sizeof(float);  // components per sample: one lane each
+  static constexpr int CPW = WG / NC;                     // chunks per workgroup
+  static constexpr int TS = CPW * kChunk;                 // samples per tile: 33 KB of LDS either way
   static constexpr int STRIDE = kChunk + 1;
   __device__ static int at(int idx) { return idx + idx / kChunk; }
 };
@@ -202,7 +204,7 @@ struct SetupArgs {
 template <int P>
 constexpr bool kTableInLds = kGroup * P * P * sizeof(double) <= 32 * 1024;
 
-template <class S, int P, int PASS>
+template <class S, int P, int PASS, bool VEC>
 __global__ __launch_bounds__(TileShape<S>::WG) void k_iir_chunks(Coeffs cf, const S* __restrict__ x,
                                                                  const S* __restrict__ xh, uint64_t n,
                                                                  const typename Acc<S>::type* __restrict__ starts,
@@ -225,10 +227,36 @@ __global__ __launch_bounds__(TileShape<S>::WG) void k_iir_chunks(Coeffs cf, cons
   }
   const uint64_t base = (uint64_t)blockIdx.x * TSh::TS;
   const uint32_t tlen = n - base < (uint64_t)TSh::TS ? (uint32_t)(n - base) : (uint32_t)TSh::TS;
-  for (int idx = t; idx < (int)tlen; idx += TSh::WG) tile[TSh::at(idx)] = x[base + idx];
+  constexpr int SPV = 16 / sizeof(S);          // samples per 16-byte load
+  constexpr int NV = TSh::TS / SPV / TSh::WG;   // 16-byte loads per thread for a whole tile
+  if (VEC && tlen == (uint32_t)TSh::TS) {
+    // every load in flight before the first LDS write (a load-then-store loop would wait on HBM
+    // latency once per iteration)
+    const float4* __restrict__ src = reinterpret_cast<const float4*>(x + base);
+    float4 v[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] = src[k * TSh::WG + t];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int idx = (k * TSh::WG + t) * SPV;  // SPV consecutive samples, all in one chunk row
+      float* d = reinterpret_cast<float*>(tile + TSh::at(idx));
+      d[0] = v[k].x;
+      d[1] = v[k].y;
+      d[2] = v[k].z;
+      d[3] = v[k].w;
+    }
+  } else {
+    for (int idx = t; idx < (int)tlen; idx += TSh::WG) tile[TSh::at(idx)] = x[base + idx];
+  }
   __syncthreads();
-  const uint64_t c = (uint64_t)blockIdx.x * TSh::WG + t;
+  // lane t runs the recursion of component t % NC of chunk t / NC (complex samples with real
+  // coefficients are two independent real recursions): scalar double state, twice the lanes
+  constexpr int NC = TSh::NC;
+  const int comp = t % NC;
+  const uint64_t c = (uint64_t)blockIdx.x * TSh::CPW + t / NC;
   const uint64_t n0 = c * kChunk;
+  const double* __restrict__ starts_d = reinterpret_cast<const double*>(starts);
+  double* __restrict__ tails_d = reinterpret_cast<double*>(tails);
   if (n0 < n) {
     const uint32_t len = n - n0 < (uint64_t)kChunk ? (uint32_t)(n - n0) : (uint32_t)kChunk;
     double b[P + 1], am[P + 1];
@@ -237,21 +265,22 @@ __global__ __launch_bounds__(TileShape<S>::WG) void k_iir_chunks(Coeffs cf, cons
       b[i] = coeff(cf.b, cf.K, i);
       am[i] = -coeff(cf.a, cf.K, i);
     }
-    S xs[P];  // x[n-1-i] (exact floats)
-    A ys[P];  // y[n-1-i]
+    float xs[P];   // component of x[n-1-i] (exact floats)
+    double ys[P];  // component of y[n-1-i]
 #pragma unroll
     for (int i = 0; i < P; ++i) {
-      xs[i] = x_at(x, xh, cf.K, (int64_t)n0 - 1 - i);
-      ys[i] = PASS == kFinal ? starts[c * P + i] : zero_s(A{});
+      const S xv = x_at(x, xh, cf.K, (int64_t)n0 - 1 - i);
+      xs[i] = reinterpret_cast<const float*>(&xv)[comp];
+      ys[i] = PASS == kFinal ? starts_d[(c * P + i) * NC + comp] : 0.0;
     }
-    S* __restrict__ row = tile + t * TSh::STRIDE;
+    float* __restrict__ row = reinterpret_cast<float*>(tile + (t / NC) * TSh::STRIDE) + comp;
     for (uint32_t k = 0; k < len; ++k) {
-      const S xv = row[k];
-      A acc = fma_s(b[0], xv, zero_s(A{}));
+      const float xv = row[k * NC];
+      double acc = b[0] * (double)xv;
 #pragma unroll
-      for (int i = 1; i <= P; ++i) acc = fma_s(b[i], xs[i - 1], acc);
+      for (int i = 1; i <= P; ++i) acc = fma(b[i], (double)xs[i - 1], acc);
 #pragma unroll
-      for (int i = 1; i <= P; ++i) acc = fma_s(am[i], ys[i - 1], acc);
+      for (int i = 1; i <= P; ++i) acc = fma(am[i], ys[i - 1], acc);
 #pragma unroll
       for (int i = P - 1; i > 0; --i) {
         xs[i] = xs[i - 1];
@@ -259,24 +288,34 @@ __global__ __launch_bounds__(TileShape<S>::WG) void k_iir_chunks(Coeffs cf, cons
       }
       xs[0] = xv;
       ys[0] = acc;
-      if constexpr (PASS == kFinal) row[k] = to_sample(acc);  // y replaces x in this thread's row
+      if constexpr (PASS == kFinal) row[k * NC] = (float)acc;  // y replaces x in this chunk's row
     }
     if constexpr (PASS == kTails) {
 #pragma unroll
-      for (int i = 0; i < P; ++i) tails[c * P + i] = ys[i];
+      for (int i = 0; i < P; ++i) tails_d[(c * P + i) * NC + comp] = ys[i];
     } else if (n0 + len == n) {
       // the last chunk's state after the call (outputs, then inputs, newest first), staged for the
       // caller's history buffers
 #pragma unroll
       for (int i = 0; i < P; ++i) {
-        tails[i] = ys[i];
-        tails[P + i] = to_acc(xs[i]);
+        tails_d[i * NC + comp] = ys[i];
+        tails_d[(P + i) * NC + comp] = xs[i];
       }
     }
   }
   if constexpr (PASS == kFinal) {
     __syncthreads();
-    for (int idx = t; idx < (int)tlen; idx += TSh::WG) y[base + idx] = tile[TSh::at(idx)];
+    if (VEC && tlen == (uint32_t)TSh::TS) {
+      float4* __restrict__ dst = reinterpret_cast<float4*>(y + base);
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const int idx = (k * TSh::WG + t) * SPV;
+        const float* d = reinterpret_cast<const float*>(tile + TSh::at(idx));
+        dst[k * TSh::WG + t] = make_float4(d[0], d[1], d[2], d[3]);
+      }
+    } else {
+      for (int idx = t; idx < (int)tlen; idx += TSh::WG) y[base + idx] = tile[TSh::at(idx)];
+    }
   }
 }
 
@@ -450,9 +489,14 @@ static hipError_t run(const Coeffs& cf, S* xh, S* yh, const S* x, S* y, uint64_t
   const int Pk = K - 1;  // live state components (<= P); the rest stay zero
 
   constexpr int WG = TileShape<S>::WG;
-  const uint32_t blocks = (uint32_t)ceil_div<uint64_t>(C, WG);
+  const uint32_t blocks = (uint32_t)ceil_div<uint64_t>(C, TileShape<S>::CPW);
   const SetupArgs sa{yh, s0, table(0), levels};
-  k_iir_chunks<S, P, kTails><<<blocks + 1, WG, 0, st>>>(cf, x, xh, n, nullptr, elems(0), nullptr, sa);
+  const bool vec = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15u) == 0;
+  if (vec) {
+    k_iir_chunks<S, P, kTails, true><<<blocks + 1, WG, 0, st>>>(cf, x, xh, n, nullptr, elems(0), nullptr, sa);
+  } else {
+    k_iir_chunks<S, P, kTails, false><<<blocks + 1, WG, 0, st>>>(cf, x, xh, n, nullptr, elems(0), nullptr, sa);
+  }
   // levels with more than kRestWaves groups: one launch each; the rest: one single-workgroup launch
   Levels<A> L{};
   for (int k = 0; k <= levels; ++k) {
@@ -474,7 +518,11 @@ static hipError_t run(const Coeffs& cf, S* xh, S* yh, const S* x, S* y, uint64_t
     k_iir_down<A, P><<<(uint32_t)ceil_div<uint64_t>(E[k], kGroup), 64, 0, st>>>(E[k], table(k), starts(k + 1),
                                                                                starts(k));
   }
-  k_iir_chunks<S, P, kFinal><<<blocks, WG, 0, st>>>(cf, x, xh, n, starts(0), st_out, y, SetupArgs{});
+  if (vec) {
+    k_iir_chunks<S, P, kFinal, true><<<blocks, WG, 0, st>>>(cf, x, xh, n, starts(0), st_out, y, SetupArgs{});
+  } else {
+    k_iir_chunks<S, P, kFinal, false><<<blocks, WG, 0, st>>>(cf, x, xh, n, starts(0), st_out, y, SetupArgs{});
+  }
   if (xh || yh) k_iir_history<S><<<1, 64, 0, st>>>(xh, yh, st_out, P, Pk);
   e = launch_status();
   const hipError_t f = hipFreeAsync(ws, st);

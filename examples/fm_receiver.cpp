@@ -5,6 +5,7 @@
 #include <gsdr/gsdr.h>
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -63,10 +64,41 @@ int main() {
   CHECK(gsdrFmDemod(fs, 0.0f, chan, dev, D, 0, dTaps, T, dX, dFm2, n1, 0, stream));
   CHECK(gsdrFmDemod(fs, 0.0f, chan, dev, D, n1 * D, dTaps, T, dX + n1 * D, dFm2 + n1, N - n1, 0, stream));
 
-  std::vector<float> fm(N), fm2(N);
+  // extensions: an int8 I/Q front end fed through the streaming object in uneven buffers, which must
+  // reproduce one gsdrxFmDemodInt8 call over the whole signal bit for bit
+  std::vector<int8_t> x8(2 * L);
+  for (size_t n = 0; n < L; ++n) {
+    x8[2 * n] = (int8_t)std::lrint(100.0f * x[n].x);
+    x8[2 * n + 1] = (int8_t)std::lrint(100.0f * x[n].y);
+  }
+  int8_t* dX8;
+  float *dFm8, *dFm8s;
+  CHECK(hipMalloc(&dX8, 2 * L));
+  CHECK(hipMalloc(&dFm8, N * sizeof(float)));
+  CHECK(hipMalloc(&dFm8s, N * sizeof(float)));
+  CHECK(hipMemcpyAsync(dX8, x8.data(), 2 * L, hipMemcpyHostToDevice, stream));
+  CHECK(gsdrxFmDemodInt8(fs, 0.0f, chan, dev, D, 0, dTaps, T, dX8, dFm8, N, 0, stream));
+  gsdrxStream rx;
+  CHECK(gsdrxStreamCreate(&rx, GSDRX_STREAM_FM, GSDRX_SAMPLES_CS8, D, dTaps, T, fs, 0.0f, chan, dev, 0, 0));
+  size_t consumed = 0, produced = 0;
+  const size_t buffers[] = {1000, 7, 123457, 50000};
+  for (size_t b = 0; consumed < L; ++b) {
+    const size_t m = std::min(buffers[b % 4], L - consumed);
+    size_t n_out = 0;
+    CHECK(gsdrxStreamProcess(rx, dX8 + 2 * consumed, m, dFm8s + produced, N - produced, &n_out, stream));
+    consumed += m;
+    produced += n_out;
+  }
+  CHECK(gsdrxStreamDestroy(rx));
+
+  std::vector<float> fm(N), fm2(N), fm8(N), fm8s(N);
   CHECK(hipMemcpyAsync(fm.data(), dFm, N * sizeof(float), hipMemcpyDeviceToHost, stream));
   CHECK(hipMemcpyAsync(fm2.data(), dFm2, N * sizeof(float), hipMemcpyDeviceToHost, stream));
+  CHECK(hipMemcpyAsync(fm8.data(), dFm8, N * sizeof(float), hipMemcpyDeviceToHost, stream));
+  CHECK(hipMemcpyAsync(fm8s.data(), dFm8s, N * sizeof(float), hipMemcpyDeviceToHost, stream));
   CHECK(hipStreamSynchronize(stream));
+  // the stream emits every output whose window has arrived: all N (the input holds N*D + T samples)
+  const bool stream_same = produced == N && std::memcmp(fm8.data(), fm8s.data(), N * sizeof(float)) == 0;
 
   double lo = 1e30, hi = -1e30;
   for (size_t i = 1000; i < N; ++i) {
@@ -76,13 +108,17 @@ int main() {
   const bool same = std::memcmp(fm.data(), fm2.data(), N * sizeof(float)) == 0;
   // gsdrFmDemod's gain is fs / (2 pi dev) at the RF rate (reference fm.cu:203), so a full-deviation
   // tone reads +-D after decimation by D
-  std::printf("%s: FM output range [%.3f, %.3f] (expect about +-%u), chunked == monolithic: %s\n", gsdrVersion(), lo,
-              hi, D, same ? "yes" : "NO");
+  std::printf("%s: FM output range [%.3f, %.3f] (expect about +-%u), chunked == monolithic: %s, "
+              "int8 stream == monolithic: %s\n",
+              gsdrVersion(), lo, hi, D, same ? "yes" : "NO", stream_same ? "yes" : "NO");
   (void)hipFree(dTaps);
   (void)hipFree(dX);
   (void)hipFree(dY);
   (void)hipFree(dFm);
   (void)hipFree(dFm2);
+  (void)hipFree(dX8);
+  (void)hipFree(dFm8);
+  (void)hipFree(dFm8s);
   (void)hipStreamDestroy(stream);
-  return same && hi > 0.8 * D && hi < 1.2 * D && lo < -0.8 * D && lo > -1.2 * D ? 0 : 1;
+  return same && stream_same && hi > 0.8 * D && hi < 1.2 * D && lo < -0.8 * D && lo > -1.2 * D ? 0 : 1;
 }

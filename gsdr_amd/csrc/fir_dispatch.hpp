@@ -61,7 +61,8 @@ hipError_t launch_generic(const FirJob& j, hipStream_t s) {
   return launch_status();
 }
 
-template <class TapT, class InT, int D, int R, int JC, int WG, int MODE, int ABL = 0, bool NT = false, bool XM = false>
+template <class TapT, class InT, int D, int R, int JC, int WG, int MODE, int ABL = 0, bool NT = false, bool XM = false,
+          int CST = 0>
 hipError_t launch_poly(const FirJob& j, hipStream_t s) {
   using Geo = TileGeo<InT, D, R, WG>;
   FirParams p = make_params(j);
@@ -79,9 +80,9 @@ hipError_t launch_poly(const FirJob& j, hipStream_t s) {
   constexpr uint64_t A = SampleT<InT>::kSrcAlign;
   const bool vec = (reinterpret_cast<uintptr_t>(j.in) % A) == 0 && ((uint64_t)stride * D * sizeof(InT)) % A == 0;
   if (vec) {
-    k_fir_poly<TapT, InT, D, R, JC, WG, true, MODE, ABL, NT, XM><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
+    k_fir_poly<TapT, InT, D, R, JC, WG, true, MODE, ABL, NT, XM, CST><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
   } else {
-    k_fir_poly<TapT, InT, D, R, JC, WG, false, MODE, ABL, NT, XM><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
+    k_fir_poly<TapT, InT, D, R, JC, WG, false, MODE, ABL, NT, XM, CST><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
   }
   return launch_status();
 }
@@ -138,6 +139,10 @@ hipError_t launch_d4_complex(const FirJob& j, hipStream_t s) {
       return launch_poly<TapT, InT, 4, 4, 16, 256, MODE>(j, s);
     case 9:  // default shape, XCD-aware tile order
       return launch_poly<TapT, InT, 4, 4, 16, 256, MODE, 0, true, true>(j, s);
+    case 10:  // default shape, tile stored through LDS (coalesced), plain stores
+      return launch_poly<TapT, InT, 4, 4, 16, 256, MODE, 0, true, false, 1>(j, s);
+    case 11:  // default shape, tile stored through LDS (coalesced), streaming stores
+      return launch_poly<TapT, InT, 4, 4, 16, 256, MODE, 0, true, false, 2>(j, s);
     case 24:
       return launch_poly<TapT, InT, 4, 4, 16, 64, MODE, 0, true>(j, s);
     case 28:

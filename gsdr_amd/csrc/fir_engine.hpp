@@ -447,6 +447,38 @@ __device__ __forceinline__ float am_env(float2 y) {
   return 2.0f * m - 1.0f;
 }
 
+// FIR-mode store of a whole tile through LDS (CST != 0): thread t holds outputs t*R .. t*R+R-1, so a
+// direct 16-byte store puts the lanes of one wave instruction R*sizeof(OutT) bytes apart (2 KB, 16
+// cache lines per instruction for complex R = 4). Transposed through LDS, slot q*WG + t of the tile
+// goes out with lane t, and every wave instruction writes one contiguous 1 KB run. CST = 2 uses
+// streaming (non-temporal) stores. Returns false (nothing written) for a partial or misaligned tile,
+// which then takes the per-thread store; the condition is uniform over the workgroup.
+template <int CST, class OutT, int R, int WG>
+__device__ __forceinline__ bool store_tile_lds(float4* lds, const FirParams& p, uint64_t out0, const OutT (&acc)[R]) {
+  constexpr int NQ = R * (int)sizeof(OutT) / 16;  // float4 per thread
+  static_assert(NQ * 16 == R * (int)sizeof(OutT), "R outputs must fill whole 16-byte slots");
+  OutT* out = reinterpret_cast<OutT*>(p.out) + out0;
+  if (out0 + (uint64_t)WG * R > p.N || (reinterpret_cast<uintptr_t>(out) & 15u) != 0) return false;
+  const uint32_t t = threadIdx.x;
+  __syncthreads();  // every wave is done reading the input tile
+  float4 w[NQ];
+  __builtin_memcpy(w, acc, sizeof(w));
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) lds[t * NQ + q] = w[q];
+  __syncthreads();
+  float4* o = reinterpret_cast<float4*>(out);
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const float4 v = lds[q * WG + t];
+    if constexpr (CST == 2) {
+      store16_nt(o + q * WG + t, v);
+    } else {
+      o[q * WG + t] = v;
+    }
+  }
+  return true;
+}
+
 // Shared by both tiled kernels. `xs` is a WG-sized LDS exchange area (FM mode only).
 template <int MODE, class OutT, int R, int WG, bool NTS = false>
 __device__ __forceinline__ void tile_epilogue(const FirParams& p, uint64_t out0, OutT (&acc)[R], float2* xs) {
@@ -542,7 +574,7 @@ __device__ __forceinline__ uint32_t tile_of_block() {
 }
 
 template <class TapT, class InT, int D, int R, int JC, int WG, bool VEC, int MODE, int ABL = 0, bool NT = false,
-          bool XM = false>
+          bool XM = false, int CST = 0>
 __global__ __launch_bounds__(WG) void k_fir_poly(FirParams p) {
   using Geo = TileGeo<InT, D, R, WG>;
   using OutT = typename Product<TapT, InT>::type;
@@ -570,6 +602,9 @@ __global__ __launch_bounds__(WG) void k_fir_poly(FirParams p) {
     poly_compute<TapT, InT, D, R, JC, WG>(lds, p, acc);
   }
 
+  if constexpr (CST != 0 && MODE == kModeFir) {
+    if (store_tile_lds<CST, OutT, R, WG>(lds, p, out0, acc)) return;
+  }
   float2* xs = reinterpret_cast<float2*>(lds + Geo::padded(NG - 1) + 1);
   tile_epilogue<MODE, OutT, R, WG, NT>(p, out0, acc, xs);
 }

@@ -31,11 +31,29 @@ __device__ __forceinline__ uint32_t qpsk_bits(float2 v) {
   return (v.x >= 0.0f ? 0u : 1u) | (v.y >= 0.0f ? 0u : 2u);
 }
 
-// grid.y = stream index
+// grid.y = stream index. A block owns kQBlock * kQSym consecutive symbols. A full, aligned block is
+// moved with lanes on consecutive 16-byte symbol pairs (each wave instruction covers 1 KB of IQ);
+// the last block keeps the thread-owns-16-symbols path below.
 __global__ __launch_bounds__(kQBlock) void k_qpsk_mod(QpskStreams st, uint32_t n, float a) {
   const uint8_t* __restrict__ in = reinterpret_cast<const uint8_t*>(st.in[blockIdx.y]);
   float2* __restrict__ out = reinterpret_cast<float2*>(st.out[blockIdx.y]);
-  const uint64_t s0 = ((uint64_t)blockIdx.x * kQBlock + threadIdx.x) * kQSym;
+  const uint64_t base = (uint64_t)blockIdx.x * kQBlock * kQSym;
+  if (base + kQBlock * kQSym <= n && (reinterpret_cast<uintptr_t>(out) & 15u) == 0) {
+    const uint8_t* bin = in + (base >> 2);
+    float4* o = reinterpret_cast<float4*>(out + base);
+    uint32_t byte[kQSym / 2];
+#pragma unroll
+    for (int q = 0; q < kQSym / 2; ++q) byte[q] = bin[(q * kQBlock + threadIdx.x) >> 1];
+#pragma unroll
+    for (int q = 0; q < kQSym / 2; ++q) {
+      const uint32_t nib = byte[q] >> (4 * (threadIdx.x & 1u));  // pair (q * kQBlock + t): symbols 2p, 2p + 1
+      const float2 p0 = qpsk_point(nib & 3u, a);
+      const float2 p1 = qpsk_point((nib >> 2) & 3u, a);
+      o[q * kQBlock + threadIdx.x] = make_float4(p0.x, p0.y, p1.x, p1.y);
+    }
+    return;
+  }
+  const uint64_t s0 = base + (uint64_t)threadIdx.x * kQSym;
   if (s0 >= n) return;
   const uint64_t b0 = s0 >> 2;
   const uint32_t nbytes = (uint32_t)((n + 3u) >> 2);
@@ -67,7 +85,27 @@ __global__ __launch_bounds__(kQBlock) void k_qpsk_mod(QpskStreams st, uint32_t n
 __global__ __launch_bounds__(kQBlock) void k_qpsk_demod(QpskStreams st, uint32_t n) {
   const float2* __restrict__ in = reinterpret_cast<const float2*>(st.in[blockIdx.y]);
   uint8_t* __restrict__ out = reinterpret_cast<uint8_t*>(st.out[blockIdx.y]);
-  const uint64_t s0 = ((uint64_t)blockIdx.x * kQBlock + threadIdx.x) * kQSym;
+  const uint64_t base = (uint64_t)blockIdx.x * kQBlock * kQSym;
+  if (base + kQBlock * kQSym <= n && (reinterpret_cast<uintptr_t>(in) & 15u) == 0 &&
+      (reinterpret_cast<uintptr_t>(out) & 3u) == 0) {
+    // lane t of slot q reads symbol pair p = q * kQBlock + t; 8 lanes assemble one 32-bit word
+    const float4* src = reinterpret_cast<const float4*>(in + base);
+    float4 v[kQSym / 2];
+#pragma unroll
+    for (int q = 0; q < kQSym / 2; ++q) v[q] = src[q * kQBlock + threadIdx.x];
+    uint32_t* dst = reinterpret_cast<uint32_t*>(out + (base >> 2));
+#pragma unroll
+    for (int q = 0; q < kQSym / 2; ++q) {
+      uint32_t w = (qpsk_bits(make_float2(v[q].x, v[q].y)) | (qpsk_bits(make_float2(v[q].z, v[q].w)) << 2))
+                   << (4 * (threadIdx.x & 7u));
+      w |= __shfl_xor(w, 1);
+      w |= __shfl_xor(w, 2);
+      w |= __shfl_xor(w, 4);
+      if ((threadIdx.x & 7u) == 0) dst[(q * kQBlock + threadIdx.x) >> 3] = w;
+    }
+    return;
+  }
+  const uint64_t s0 = base + (uint64_t)threadIdx.x * kQSym;
   if (s0 >= n) return;
   const uint64_t b0 = s0 >> 2;
   uint32_t word = 0;

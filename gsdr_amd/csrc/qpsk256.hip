@@ -127,7 +127,24 @@ __global__ __launch_bounds__(kCBlock) void k_c256_mod(C256Streams st, uint32_t n
   load_table(tab, type);
   const uint8_t* __restrict__ in = reinterpret_cast<const uint8_t*>(st.in[blockIdx.y]);
   float2* __restrict__ out = reinterpret_cast<float2*>(st.out[blockIdx.y]);
-  const uint64_t s0 = ((uint64_t)blockIdx.x * kCBlock + threadIdx.x) * kCSym;
+  // a full, aligned block: lane t of slot q handles symbol pair q * kCBlock + t (coalesced 1 KB stores)
+  const uint64_t base = (uint64_t)blockIdx.x * kCBlock * kCSym;
+  if (base + kCBlock * kCSym <= n && (reinterpret_cast<uintptr_t>(in) & 1u) == 0 &&
+      (reinterpret_cast<uintptr_t>(out) & 15u) == 0) {
+    const uint16_t* pin = reinterpret_cast<const uint16_t*>(in + base);
+    float4* o = reinterpret_cast<float4*>(out + base);
+    uint32_t pr[kCSym / 2];
+#pragma unroll
+    for (int q = 0; q < kCSym / 2; ++q) pr[q] = pin[q * kCBlock + threadIdx.x];
+#pragma unroll
+    for (int q = 0; q < kCSym / 2; ++q) {
+      const float2 p0 = tab[pr[q] & 0xffu];
+      const float2 p1 = tab[pr[q] >> 8];
+      o[q * kCBlock + threadIdx.x] = make_float4(p0.x, p0.y, p1.x, p1.y);
+    }
+    return;
+  }
+  const uint64_t s0 = base + (uint64_t)threadIdx.x * kCSym;
   if (s0 >= n) return;
   if (s0 + kCSym <= n && (reinterpret_cast<uintptr_t>(in + s0) & 15u) == 0 &&
       (reinterpret_cast<uintptr_t>(out + s0) & 15u) == 0) {
@@ -168,7 +185,8 @@ __global__ __launch_bounds__(kCBlock) void k_c256_demod(C256Streams st, uint32_t
   __syncthreads();
   const float2* __restrict__ in = reinterpret_cast<const float2*>(st.in[blockIdx.y]);
   uint8_t* __restrict__ out = reinterpret_cast<uint8_t*>(st.out[blockIdx.y]);
-  const uint64_t s0 = ((uint64_t)blockIdx.x * kCBlock + threadIdx.x) * kCSym;
+  const uint64_t base = (uint64_t)blockIdx.x * kCBlock * kCSym;
+  const uint64_t s0 = base + (uint64_t)threadIdx.x * kCSym;
   if (s0 >= n) return;
   const float a = tab[255].x;  // rectangular: (15 - 7.5) / 7.5 * a == a exactly
   const float scale = 7.5f / a;
@@ -199,6 +217,22 @@ __global__ __launch_bounds__(kCBlock) void k_c256_demod(C256Streams st, uint32_t
     }
     return demod_exhaustive(tab, r);
   };
+  if (base + kCBlock * kCSym <= n && (reinterpret_cast<uintptr_t>(in) & 15u) == 0 &&
+      (reinterpret_cast<uintptr_t>(out) & 1u) == 0) {
+    // full, aligned block: lane t of slot q reads symbol pair q * kCBlock + t (coalesced 1 KB loads)
+    const float4* src = reinterpret_cast<const float4*>(in + base);
+    uint16_t* dst = reinterpret_cast<uint16_t*>(out + base);
+    float4 v[kCSym / 2];
+#pragma unroll
+    for (int q = 0; q < kCSym / 2; ++q) v[q] = src[q * kCBlock + threadIdx.x];
+#pragma unroll
+    for (int q = 0; q < kCSym / 2; ++q) {
+      const uint32_t i0 = demod(make_float2(v[q].x, v[q].y));
+      const uint32_t i1 = demod(make_float2(v[q].z, v[q].w));
+      dst[q * kCBlock + threadIdx.x] = (uint16_t)(i0 | (i1 << 8));
+    }
+    return;
+  }
   if (s0 + kCSym <= n && (reinterpret_cast<uintptr_t>(in + s0) & 15u) == 0 &&
       (reinterpret_cast<uintptr_t>(out + s0) & 15u) == 0) {
     const float4* src = reinterpret_cast<const float4*>(in + s0);

@@ -110,7 +110,7 @@ def test_fir_restores_current_device(cuda):
     assert torch.cuda.current_device() == 0
 
 
-@pytest.mark.parametrize("variant", [0, 1, 3, 4, 5, 7, 8, 9, 24, 28])
+@pytest.mark.parametrize("variant", [0, 1, 3, 4, 5, 7, 8, 9, 10, 11, 24, 28])
 def test_fir_fc_d4_variants(cuda, variant):
     """Every tile shape of the headline kernel (gsdrxFirFCVariant) meets the same bar."""
     from gsdr_amd import ops
@@ -121,6 +121,22 @@ def test_fir_fc_d4_variants(cuda, variant):
     torch.cuda.synchronize()
     ref = o.fir(taps, x, D, N)
     assert normwise_err(y.cpu().numpy(), ref, bound(taps, x, D, N)) <= FLOAT_TOL
+
+
+@pytest.mark.parametrize("variant", [9, 10, 11])
+@pytest.mark.parametrize("N", [1024, 50000 + 3, 3 * 1024 + 1])
+def test_fir_fc_d4_store_variants_bit_identical(cuda, variant, N):
+    """Variants that change only the tile order or the store path (XCD order, LDS-transposed stores)
+    keep the default's per-output MAC order: outputs equal variant 0 bit for bit, tails included."""
+    from gsdr_amd import ops
+
+    D, T = 4, 127
+    taps, x = make("FC", T, (N - 1) * D + T, 5)
+    tt, xt = dev(taps, cuda), dev(x, cuda)
+    y0 = ops.fir_variant(0, tt, xt, D, N)
+    y = ops.fir_variant(variant, tt, xt, D, N)
+    torch.cuda.synchronize()
+    assert np.array_equal(y.cpu().numpy().view(np.uint64), y0.cpu().numpy().view(np.uint64))
 
 
 def test_fir_fc_d4_full_config(cuda):

@@ -198,3 +198,45 @@ def test_qpsk256_circular_cells_bit_exact_dense(cuda, amp):
     rx = (rng.uniform(-span, span, n) + 1j * rng.uniform(-span, span, n)).astype(np.complex64)
     got = ops.qpsk256_demodulate(dev(rx, cuda), 1).cpu().numpy()
     assert np.array_equal(got, o.qpsk256_demod(table, rx))
+
+
+@pytest.mark.parametrize("ctype", [0, 1])
+@pytest.mark.parametrize("in_off,out_off", [(0, 0), (1, 0), (0, 1), (1, 1)])
+def test_qpsk256_blocks_and_alignment(cuda, ctype, in_off, out_off):
+    """Several whole 4096-symbol blocks plus a ragged tail, with the input or output pointer offset
+    by one element: the coalesced block path and the per-thread path must agree with the oracle."""
+    from gsdr_amd import ops
+
+    n = 3 * 4096 + 77
+    ops.qpsk256_init(ctype, 1.0)
+    table = o.qpsk256_table(ctype, 1.0)
+    rng = np.random.default_rng(17 + ctype)
+    syms = rng.integers(0, 256, n + 1, dtype=np.uint8)
+    sym_t = dev(syms, cuda)[in_off:in_off + n]
+    out = torch.empty(n + 1, dtype=torch.complex64, device=cuda)[out_off:out_off + n]
+    ops.qpsk256_modulate(sym_t, ctype, out=out)
+    assert np.array_equal(out.cpu().numpy(), o.qpsk256_mod(table, syms[in_off:in_off + n]))
+    rx = (o.qpsk256_mod(table, syms[:n + 1]) + 0.01 * (rng.standard_normal(n + 1) + 1j * rng.standard_normal(n + 1)))
+    rx = rx.astype(np.complex64)
+    got = torch.empty(n + 1, dtype=torch.uint8, device=cuda)[out_off:out_off + n]
+    ops.qpsk256_demodulate(dev(rx, cuda)[in_off:in_off + n], ctype, out=got)
+    assert np.array_equal(got.cpu().numpy(), o.qpsk256_demod(table, rx[in_off:in_off + n]))
+
+
+@pytest.mark.parametrize("out_off", [0, 1, 2])
+def test_qpsk_blocks_and_alignment(cuda, out_off):
+    """Whole 4096-symbol blocks plus a tail, output (modulate) / bit (demodulate) pointers offset."""
+    from gsdr_amd import ops
+
+    n = 5 * 4096 + 13
+    nb = (n + 3) // 4
+    rng = np.random.default_rng(out_off)
+    bits = rng.integers(0, 256, nb, dtype=np.uint8)
+    out = torch.empty(n + 2, dtype=torch.complex64, device=cuda)[out_off:out_off + n]
+    ops.qpsk_modulate(dev(bits, cuda), n, 0.75, out=out)
+    sym = o.qpsk_mod(bits, n, 0.75)
+    assert np.array_equal(out.cpu().numpy(), sym)
+    _, rx = noisy_qpsk(bits, n, 1.0, 3)
+    got = torch.full((nb + 2,), 0x5A, dtype=torch.uint8, device=cuda)[out_off:out_off + nb]
+    ops.qpsk_demodulate(dev(rx, cuda), n, out=got)
+    assert np.array_equal(got.cpu().numpy(), o.qpsk_demod(rx, n, initial=np.full(nb, 0x5A, np.uint8)))

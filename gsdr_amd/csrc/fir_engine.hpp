@@ -279,28 +279,53 @@ __device__ __forceinline__ float4 load_granule(const InT* __restrict__ in, uint6
   return r;
 }
 
-// s = local sample index (only its low 32 bits matter: the NCO phase is taken mod 2^32).
-// s = local sample index of a granule's first sample (only its low 32 bits matter).
+// NCO mixing of one granule (two complex samples n, n + 1) given ph = n * inc mod 2^32, the phase of
+// its first sample; `odd` = n & 1 (wave-uniform in the tiled kernels: they stage granules at even
+// offsets from the tile start). The phasor is a pure function of the absolute index: even n from
+// nco_direct, odd n = phasor(n - 1) * w, w = nco_direct(inc).
 template <class InT, int MODE>
-__device__ __forceinline__ float4 stage_transform(float4 v, uint32_t s, const FirParams& p) {
+__device__ __forceinline__ float4 stage_transform_ph(float4 v, uint32_t ph, bool odd, uint32_t inc) {
   if constexpr (MODE != kModeFir) {
     static_assert(SampleT<InT>::kPerGranule == 2, "NCO modes take complex input");
-    const uint32_t n = p.nco_n0 + s;  // absolute index of the granule's first sample mod 2^32
-    const float2 w = nco_direct(p.nco_inc);
+    const float2 w = nco_direct(inc);
     float2 ea, eb;
-    // wave-uniform: the tiled kernels stage granules at even offsets from an even-or-odd tile start
-    if (__builtin_amdgcn_readfirstlane(n & 1u) == 0) {
-      ea = nco_direct(n * p.nco_inc);
-      eb = cmul(ea, w);
+    if (odd) {
+      ea = cmul(nco_direct(ph - inc), w);
+      eb = nco_direct(ph + inc);
     } else {
-      ea = cmul(nco_direct((n - 1u) * p.nco_inc), w);
-      eb = nco_direct((n + 1u) * p.nco_inc);
+      ea = nco_direct(ph);
+      eb = cmul(ea, w);
     }
     const float2 a = cmul(make_float2(v.x, v.y), ea);
     const float2 b = cmul(make_float2(v.z, v.w), eb);
     v = make_float4(a.x, a.y, b.x, b.y);
   }
   return v;
+}
+
+// s = local sample index of a granule's first sample (only its low 32 bits matter: the NCO phase is
+// taken mod 2^32).
+template <class InT, int MODE>
+__device__ __forceinline__ float4 stage_transform(float4 v, uint32_t s, const FirParams& p) {
+  if constexpr (MODE != kModeFir) {
+    const uint32_t n = p.nco_n0 + s;  // absolute index of the granule's first sample mod 2^32
+    return stage_transform_ph<InT, MODE>(v, n * p.nco_inc, __builtin_amdgcn_readfirstlane(n & 1u) != 0, p.nco_inc);
+  }
+  return v;
+}
+
+// Phase walk of a thread's tile-body granules: granule g = k * WG + tid of a tile starting at S0 has
+// phase ph0 + k * step (mod 2^32) -- the same integer as (n0 + S0 + g * G) * inc, so the phasors
+// are unchanged, without a 32-bit integer multiply (a quarter-rate instruction) per granule.
+struct PhaseWalk {
+  uint32_t ph0, step, inc;
+  bool odd;
+};
+
+template <int G, int WG>
+__device__ __forceinline__ PhaseWalk phase_walk(uint32_t n0, uint64_t S0, uint32_t inc) {
+  const uint32_t n = n0 + (uint32_t)S0 + (uint32_t)(threadIdx.x * G);
+  return PhaseWalk{n * inc, (uint32_t)(WG * G) * inc, inc, __builtin_amdgcn_readfirstlane(n & 1u) != 0};
 }
 
 // granules per staging batch: the largest divisor of the per-thread count that is at most 8
@@ -325,6 +350,7 @@ __device__ __forceinline__ void stage_tile(float4* __restrict__ lds, const InT* 
   constexpr int SB = staging_batch(BPT);
   static_assert(BPT % SB == 0, "segment granules must split into whole staging batches");
   const uint32_t tid = threadIdx.x;
+  const PhaseWalk pw = phase_walk<G, WG>(p.nco_n0, S0, p.nco_inc);
   // wave-uniform: is the whole staged span readable? (every tile but the last)
   const bool whole = VEC && (S0 + (uint64_t)NG * G <= p.L);
 #pragma unroll
@@ -360,7 +386,7 @@ __device__ __forceinline__ void stage_tile(float4* __restrict__ lds, const InT* 
 #pragma unroll
     for (int k = 0; k < SB; ++k) {
       const uint32_t g = (b0 + k) * WG + tid;
-      lds[Geo::padded(g)] = stage_transform<InT, MODE>(v[k], (uint32_t)S0 + g * G, p);
+      lds[Geo::padded(g)] = stage_transform_ph<InT, MODE>(v[k], pw.ph0 + (uint32_t)(b0 + k) * pw.step, pw.odd, pw.inc);
     }
   }
   for (uint32_t g = BPT * WG + tid; g < NG; g += WG) {
@@ -671,10 +697,11 @@ __global__ __launch_bounds__(WG) void k_fir_multi(FirParams p, MultiParams mp) {
     pc.nco_inc = mp.inc[c];
     pc.fm_gain = mp.gain[c];
     pc.out = reinterpret_cast<float*>(p.out) + (uint64_t)c * p.N;
+    const PhaseWalk pw = phase_walk<G, WG>(p.nco_n0, S0, pc.nco_inc);
 #pragma unroll
     for (int k = 0; k < BPT; ++k) {
       const uint32_t g = k * WG + tid;
-      lds[Geo::padded(g)] = stage_transform<InT, MODE>(body[k], (uint32_t)S0 + g * G, pc);
+      lds[Geo::padded(g)] = stage_transform_ph<InT, MODE>(body[k], pw.ph0 + (uint32_t)k * pw.step, pw.odd, pw.inc);
     }
 #pragma unroll
     for (int k = 0; k < HMAX; ++k) {

@@ -38,8 +38,9 @@ __constant__ float2 c_qpsk256_tables[2][256];
 // distance of any table point over the cell (plus a margin for float rounding), so every point that
 // can win the argmin anywhere in the cell -- ties included -- is on the list, and the argmin over the
 // list in index order with the same sqdist() is the exhaustive one. R == 0 disables the lookup.
-constexpr int kCellGrid = 48;
-constexpr int kMaxCellEntries = 8192;
+constexpr int kCellGrid = 96;
+constexpr int kMaxCellEntries = 19456;  // 18,764 used by the circular table (any amplitude); LDS < 40 KB
+constexpr double kCellSpan = 1.3;  // grid half-width R = 1.3 * max |c|: noisy symbols stay on the grid
 struct CircCells {
   float R;
   float inv_cs;  // kCellGrid / (2 R)
@@ -80,12 +81,20 @@ __device__ __forceinline__ int nearest_level(float v, float scale) {
 }
 
 // Rectangular fast path. Table entry 16 i + q is (lx[i], ly[q]) -- the I coordinate depends on i only
-// and the Q coordinate on q only (qpsk256.cu:33-34) -- so the 9 candidate distances are sums of 3 + 3
-// per-axis squares read from per-axis level arrays, bit-identical to sqdist() on the table entries.
-// Candidates are compared in ascending index order (i major, q minor) with strict '<'; a level
-// outside [0, 15] contributes +inf and never wins. Returns 256 when the symbol needs the exhaustive
+// and the Q coordinate on q only (qpsk256.cu:33-34) -- so every candidate distance is a rounded sum
+// fl(ex[i] + ey[q]) of per-axis squares read from level arrays, bit-identical to sqdist() on the
+// table entries. lxp / lyp are the level arrays padded with +inf at both ends (entry k + 1 = level k),
+// so neighbours outside [0, 15] have infinite distance and never win.
+//
+// The 3 x 3 neighbourhood of the per-axis nearest levels contains the exhaustive argmin for
+// |re|,|im| <= 4|a|. Rounded addition is monotone in each operand, so with a = first argmin of ex and
+// b = first argmin of ey the minimum is dmin = fl(ex[a] + ey[b]), and (a, b) is the ONLY candidate
+// reaching it when the second-smallest ex plus ey[b], and ex[a] plus the second-smallest ey, both
+// exceed dmin (any other candidate is >= one of those two sums). Then it is the exhaustive answer;
+// otherwise (a rounding tie near a decision boundary) the 9 candidates are scanned in index order
+// with strict '<', as the exhaustive search does. Returns 256 when the symbol needs the exhaustive
 // search (outside |re|,|im| <= 4|a|, or NaN).
-__device__ __forceinline__ uint32_t demod_rect_fast(const float* __restrict__ lx, const float* __restrict__ ly, float2 r,
+__device__ __forceinline__ uint32_t demod_rect_fast(const float* __restrict__ lxp, const float* __restrict__ lyp, float2 r,
                                                     float lim, float scale) {
   if (!(fabsf(r.x) <= lim && fabsf(r.y) <= lim)) return 256u;
   const int i0 = nearest_level(r.x, scale);
@@ -93,13 +102,18 @@ __device__ __forceinline__ uint32_t demod_rect_fast(const float* __restrict__ lx
   float ex[3], ey[3];
 #pragma unroll
   for (int d = 0; d < 3; ++d) {
-    const int i = i0 - 1 + d, q = q0 - 1 + d;
-    const float cx = lx[i < 0 ? 0 : (i > 15 ? 15 : i)];
-    const float cy = ly[q < 0 ? 0 : (q > 15 ? 15 : q)];
-    const float dx = __fsub_rn(r.x, cx), dy = __fsub_rn(r.y, cy);
-    ex[d] = (i < 0 || i > 15) ? INFINITY : __fmul_rn(dx, dx);
-    ey[d] = (q < 0 || q > 15) ? INFINITY : __fmul_rn(dy, dy);
+    const float dx = __fsub_rn(r.x, lxp[i0 + d]), dy = __fsub_rn(r.y, lyp[q0 + d]);
+    ex[d] = __fmul_rn(dx, dx);
+    ey[d] = __fmul_rn(dy, dy);
   }
+  const float exm = fminf(fminf(ex[0], ex[1]), ex[2]);
+  const float eym = fminf(fminf(ey[0], ey[1]), ey[2]);
+  const float ex2 = __builtin_amdgcn_fmed3f(ex[0], ex[1], ex[2]);
+  const float ey2 = __builtin_amdgcn_fmed3f(ey[0], ey[1], ey[2]);
+  const int a = ex[0] == exm ? 0 : (ex[1] == exm ? 1 : 2);
+  const int b = ey[0] == eym ? 0 : (ey[1] == eym ? 1 : 2);
+  const float dmin = __fadd_rn(exm, eym);
+  if (__fadd_rn(ex2, eym) > dmin && __fadd_rn(exm, ey2) > dmin) return (uint32_t)((i0 - 1 + a) * 16 + (q0 - 1 + b));
   float best = INFINITY;
   uint32_t idx = 0;
 #pragma unroll
@@ -165,18 +179,22 @@ __global__ __launch_bounds__(kCBlock) void k_c256_mod(C256Streams st, uint32_t n
   }
 }
 
-__global__ __launch_bounds__(kCBlock) void k_c256_demod(C256Streams st, uint32_t n, uint32_t type) {
+// TYPE 0: rectangular table (per-axis fast path); TYPE 1: circular table (per-cell candidate lists).
+// Both fall back to the exhaustive search for inputs their fast path does not cover.
+template <int TYPE>
+__global__ __launch_bounds__(kCBlock) void k_c256_demod(C256Streams st, uint32_t n) {
   __shared__ float2 tab[256];
-  __shared__ float lx[16], ly[16];
-  __shared__ uint16_t cstart[kCellGrid * kCellGrid + 1];
-  __shared__ uint8_t cidx[kMaxCellEntries];
-  const float2* tsrc = c_qpsk256_tables[type == 0 ? 0 : 1];
+  __shared__ float lxp[18], lyp[18];  // rectangular levels, padded with +inf (demod_rect_fast)
+  __shared__ uint16_t cstart[TYPE == 0 ? 1 : kCellGrid * kCellGrid + 1];
+  __shared__ uint8_t cidx[TYPE == 0 ? 4 : kMaxCellEntries];
+  const float2* tsrc = c_qpsk256_tables[TYPE];
   for (uint32_t i = threadIdx.x; i < 256; i += kCBlock) tab[i] = tsrc[i];
-  if (threadIdx.x < 16) {
-    lx[threadIdx.x] = tsrc[threadIdx.x * 16].x;
-    ly[threadIdx.x] = tsrc[threadIdx.x].y;
+  if (TYPE == 0 && threadIdx.x < 18) {
+    const int k = (int)threadIdx.x - 1;
+    lxp[threadIdx.x] = (k < 0 || k > 15) ? INFINITY : tsrc[k * 16].x;
+    lyp[threadIdx.x] = (k < 0 || k > 15) ? INFINITY : tsrc[k].y;
   }
-  if (type != 0 && g_circ_cells.R > 0.0f) {  // the circular candidate lists, into LDS
+  if (TYPE != 0 && g_circ_cells.R > 0.0f) {  // the circular candidate lists, into LDS
     for (uint32_t i = threadIdx.x; i <= (uint32_t)(kCellGrid * kCellGrid); i += kCBlock) cstart[i] = g_circ_cells.start[i];
     const uint32_t total = g_circ_cells.start[kCellGrid * kCellGrid];
     const uint32_t* src = reinterpret_cast<const uint32_t*>(g_circ_cells.idx);
@@ -185,74 +203,80 @@ __global__ __launch_bounds__(kCBlock) void k_c256_demod(C256Streams st, uint32_t
   __syncthreads();
   const float2* __restrict__ in = reinterpret_cast<const float2*>(st.in[blockIdx.y]);
   uint8_t* __restrict__ out = reinterpret_cast<uint8_t*>(st.out[blockIdx.y]);
-  const uint64_t base = (uint64_t)blockIdx.x * kCBlock * kCSym;
-  const uint64_t s0 = base + (uint64_t)threadIdx.x * kCSym;
-  if (s0 >= n) return;
-  const float a = tab[255].x;  // rectangular: (15 - 7.5) / 7.5 * a == a exactly
-  const float scale = 7.5f / a;
-  // the fast paths need a finite, non-zero amplitude (else every symbol takes the exhaustive search)
-  const float lim = (type == 0 && isfinite(scale)) ? 4.0f * fabsf(a) : -1.0f;
-  const float cR = type == 0 ? 0.0f : g_circ_cells.R;
-  const float inv_cs = g_circ_cells.inv_cs;
-  auto demod = [&](float2 r) -> uint32_t {
-    if (type == 0) {
-      const uint32_t k = demod_rect_fast(lx, ly, r, lim, scale);
-      return k < 256u ? k : demod_exhaustive(tab, r);
-    }
-    const float fx = (r.x + cR) * inv_cs, fy = (r.y + cR) * inv_cs;
-    if (cR > 0.0f && fx >= 0.0f && fy >= 0.0f && fx < (float)kCellGrid && fy < (float)kCellGrid) {
-      const int c = (int)fy * kCellGrid + (int)fx;
-      const uint32_t b = cstart[c], e = cstart[c + 1];
-      float best = INFINITY;
-      uint32_t idx = 0;
-      for (uint32_t m = b; m < e; ++m) {
-        const uint32_t k = cidx[m];
-        const float d = sqdist(r, tab[k]);
-        if (d < best) {  // ascending list: first index wins ties, as the exhaustive search
-          best = d;
-          idx = k;
-        }
-      }
-      return idx;
-    }
-    return demod_exhaustive(tab, r);
-  };
-  if (base + kCBlock * kCSym <= n && (reinterpret_cast<uintptr_t>(in) & 15u) == 0 &&
-      (reinterpret_cast<uintptr_t>(out) & 1u) == 0) {
-    // full, aligned block: lane t of slot q reads symbol pair q * kCBlock + t (coalesced 1 KB loads)
-    const float4* src = reinterpret_cast<const float4*>(in + base);
-    uint16_t* dst = reinterpret_cast<uint16_t*>(out + base);
-    float4 v[kCSym / 2];
-#pragma unroll
-    for (int q = 0; q < kCSym / 2; ++q) v[q] = src[q * kCBlock + threadIdx.x];
-#pragma unroll
-    for (int q = 0; q < kCSym / 2; ++q) {
-      const uint32_t i0 = demod(make_float2(v[q].x, v[q].y));
-      const uint32_t i1 = demod(make_float2(v[q].z, v[q].w));
-      dst[q * kCBlock + threadIdx.x] = (uint16_t)(i0 | (i1 << 8));
-    }
-    return;
-  }
-  if (s0 + kCSym <= n && (reinterpret_cast<uintptr_t>(in + s0) & 15u) == 0 &&
-      (reinterpret_cast<uintptr_t>(out + s0) & 15u) == 0) {
-    const float4* src = reinterpret_cast<const float4*>(in + s0);
-    float4 v[kCSym / 2];
-#pragma unroll
-    for (int q = 0; q < kCSym / 2; ++q) v[q] = src[q];
-    uint32_t words[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int q = 0; q < kCSym / 2; ++q) {
-      const uint32_t i0 = demod(make_float2(v[q].x, v[q].y));
-      const uint32_t i1 = demod(make_float2(v[q].z, v[q].w));
-      words[q / 2] |= (i0 | (i1 << 8)) << (16 * (q & 1));
-    }
-    *reinterpret_cast<uint4*>(out + s0) = make_uint4(words[0], words[1], words[2], words[3]);
+  float lim = -1.0f, scale = 0.0f, cR = 0.0f, inv_cs = 0.0f;
+  if constexpr (TYPE == 0) {
+    const float a = tab[255].x;  // rectangular: (15 - 7.5) / 7.5 * a == a exactly
+    scale = 7.5f / a;
+    // the fast path needs a finite, non-zero amplitude (else every symbol takes the exhaustive search)
+    lim = isfinite(scale) ? 4.0f * fabsf(a) : -1.0f;
   } else {
-    for (int k = 0; k < kCSym; ++k) {
-      if (s0 + k < n) out[s0 + k] = (uint8_t)demod(in[s0 + k]);
+    cR = g_circ_cells.R;
+    inv_cs = g_circ_cells.inv_cs;
+  }
+  auto demod = [&](float2 r) -> uint32_t {
+    if constexpr (TYPE == 0) {
+      const uint32_t k = demod_rect_fast(lxp, lyp, r, lim, scale);
+      return k < 256u ? k : demod_exhaustive(tab, r);
+    } else {
+      const float fx = (r.x + cR) * inv_cs, fy = (r.y + cR) * inv_cs;
+      if (cR > 0.0f && fx >= 0.0f && fy >= 0.0f && fx < (float)kCellGrid && fy < (float)kCellGrid) {
+        const int c = (int)fy * kCellGrid + (int)fx;
+        const uint32_t b = cstart[c], e = cstart[c + 1];
+        float best = INFINITY;
+        uint32_t idx = 0;
+        // four candidates per step with independent LDS loads; slots past the list end repeat its
+        // last entry, which cannot win again under strict '<'
+        for (uint32_t m = b; m < e; m += 4) {
+          uint32_t k[4];
+          float2 pt[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) k[j] = cidx[m + j < e ? m + j : e - 1];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) pt[j] = tab[k[j]];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float d = sqdist(r, pt[j]);
+            if (d < best) {  // ascending list: first index wins ties, as the exhaustive search
+              best = d;
+              idx = k[j];
+            }
+          }
+        }
+        return idx;
+      }
+      return demod_exhaustive(tab, r);
+    }
+  };
+  // grid-stride over 4096-symbol tiles, so the LDS tables are staged once per workgroup
+  const uint32_t tiles = (uint32_t)((n + (uint64_t)kCBlock * kCSym - 1) / ((uint64_t)kCBlock * kCSym));
+  const bool aligned = (reinterpret_cast<uintptr_t>(in) & 15u) == 0 && (reinterpret_cast<uintptr_t>(out) & 1u) == 0;
+  for (uint32_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+    const uint64_t base = (uint64_t)tile * kCBlock * kCSym;
+    if (aligned && base + kCBlock * kCSym <= n) {
+      // full, aligned tile: lane t of slot q reads symbol pair q * kCBlock + t (coalesced 1 KB loads)
+      const float4* src = reinterpret_cast<const float4*>(in + base);
+      uint16_t* dst = reinterpret_cast<uint16_t*>(out + base);
+      float4 v[kCSym / 2];
+#pragma unroll
+      for (int q = 0; q < kCSym / 2; ++q) v[q] = src[q * kCBlock + threadIdx.x];
+#pragma unroll
+      for (int q = 0; q < kCSym / 2; ++q) {
+        const uint32_t i0 = demod(make_float2(v[q].x, v[q].y));
+        const uint32_t i1 = demod(make_float2(v[q].z, v[q].w));
+        dst[q * kCBlock + threadIdx.x] = (uint16_t)(i0 | (i1 << 8));
+      }
+    } else {
+      // last tile or misaligned pointers: one symbol at a time, thread t owning symbols s0 .. s0 + 15
+      const uint64_t s0 = base + (uint64_t)threadIdx.x * kCSym;
+      for (int k = 0; k < kCSym; ++k) {
+        if (s0 + k < n) out[s0 + k] = (uint8_t)demod(in[s0 + k]);
+      }
     }
   }
 }
+
+// circular demodulation workgroups per stream (grid-stride): 4 resident per CU x 256 CUs
+constexpr uint32_t kCircBlocks = 1024;
 
 static hipError_t c256_launch(bool modulate, const C256Streams& st, int nstreams, uint32_t n, uint32_t type,
                               int32_t device, hipStream_t stream) {
@@ -267,7 +291,14 @@ static hipError_t c256_launch(bool modulate, const C256Streams& st, int nstreams
   if (modulate) {
     k_c256_mod<<<grid, dim3(kCBlock), 0, stream>>>(st, n, type);
   } else {
-    k_c256_demod<<<grid, dim3(kCBlock), 0, stream>>>(st, n, type);
+    // rectangular: one workgroup per tile; circular: one resident round of workgroups (its cell lists
+    // take < 40 KB of LDS, 4 workgroups per CU) striding over the tiles
+    const dim3 dgrid(type == 0 ? blocks : std::min<uint32_t>(blocks, kCircBlocks), (uint32_t)nstreams);
+    if (type == 0) {
+      k_c256_demod<0><<<dgrid, dim3(kCBlock), 0, stream>>>(st, n);
+    } else {
+      k_c256_demod<1><<<dgrid, dim3(kCBlock), 0, stream>>>(st, n);
+    }
   }
   return launch_status();
 }
@@ -311,7 +342,7 @@ static bool build_cells(const float2* t, CircCells* cc) {
   for (int i = 0; i < 256; ++i) rmax = std::max(rmax, std::hypot((double)t[i].x, (double)t[i].y));
   cc->R = 0.0f;
   if (!(rmax > 0.0) || !std::isfinite(rmax)) return true;  // degenerate table: exhaustive search
-  const float R = (float)(rmax * 1.02);
+  const float R = (float)(rmax * kCellSpan);
   const float inv_cs = (float)kCellGrid / (2.0f * R);
   const double cs = 1.0 / (double)inv_cs;
   const double margin = 1e-4 * rmax;  // >> float rounding of positions and distances
@@ -319,18 +350,19 @@ static bool build_cells(const float2* t, CircCells* cc) {
   for (int iy = 0; iy < kCellGrid; ++iy) {
     for (int ix = 0; ix < kCellGrid; ++ix) {
       const double x0 = -(double)R + ix * cs, x1 = x0 + cs, y0 = -(double)R + iy * cs, y1 = y0 + cs;
-      double bound = INFINITY;
+      double bound2 = INFINITY;  // smallest worst-case squared distance of a point over the cell
       for (int q = 0; q < 256; ++q) {
         const double dx = std::max(std::fabs(t[q].x - x0), std::fabs(t[q].x - x1));
         const double dy = std::max(std::fabs(t[q].y - y0), std::fabs(t[q].y - y1));
-        bound = std::min(bound, std::hypot(dx, dy));
+        bound2 = std::min(bound2, dx * dx + dy * dy);
       }
-      bound += margin;
+      const double bound = std::sqrt(bound2) + margin;
+      const double lim2 = bound * bound;
       cc->start[iy * kCellGrid + ix] = (uint16_t)n;
       for (int p = 0; p < 256; ++p) {
         const double dx = std::max({x0 - t[p].x, 0.0, t[p].x - x1});
         const double dy = std::max({y0 - t[p].y, 0.0, t[p].y - y1});
-        if (std::hypot(dx, dy) <= bound) {
+        if (dx * dx + dy * dy <= lim2) {
           if (n >= kMaxCellEntries) {
             cc->R = 0.0f;
             return true;  // does not fit: keep the exhaustive search
@@ -360,7 +392,7 @@ GSDR_C_LINKAGE hipError_t gsdrQpsk256InitConstellation(uint32_t constellationTyp
   hipError_t st = hipMemcpyToSymbolAsync(HIP_SYMBOL(gsdr::c_qpsk256_tables), table, sizeof(table), offset,
                                          hipMemcpyHostToDevice, cudaStream);
   if (st != hipSuccess) return st;
-  static thread_local gsdr::CircCells cells;  // host staging (8 KiB+): waited for below
+  static thread_local gsdr::CircCells cells;  // host staging (~38 KiB): waited for below
   if (constellationType != 0) {
     gsdr::build_cells(table, &cells);
     st = hipMemcpyToSymbolAsync(HIP_SYMBOL(gsdr::g_circ_cells), &cells, sizeof(cells), 0, hipMemcpyHostToDevice,

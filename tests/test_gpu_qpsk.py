@@ -187,13 +187,14 @@ def test_qpsk256_config5_round_trip(cuda):
 @pytest.mark.parametrize("amp", [1.0, 0.37, -2.5])
 def test_qpsk256_circular_cells_bit_exact_dense(cuda, amp):
     """The circular table's per-cell candidate lists (qpsk256.hip CircCells) reproduce the exhaustive
-    argmin bit for bit: 4 M points uniform over a square larger than the grid (outside -> exhaustive)."""
+    argmin bit for bit: 5.4 M points uniform over a square larger than the grid (outside -> exhaustive);
+    more 4096-symbol tiles than demodulation workgroups, so the grid-stride loop and the tail run."""
     from gsdr_amd import ops
 
     ops.qpsk256_init(1, amp)
     table = o.qpsk256_table(1, amp)
     rng = np.random.default_rng(int(abs(amp) * 100))
-    n = 1 << 22
+    n = (1 << 22) + 4096 * 300 + 7
     span = 2.2 * abs(amp)
     rx = (rng.uniform(-span, span, n) + 1j * rng.uniform(-span, span, n)).astype(np.complex64)
     got = ops.qpsk256_demodulate(dev(rx, cuda), 1).cpu().numpy()
@@ -240,3 +241,27 @@ def test_qpsk_blocks_and_alignment(cuda, out_off):
     got = torch.full((nb + 2,), 0x5A, dtype=torch.uint8, device=cuda)[out_off:out_off + nb]
     ops.qpsk_demodulate(dev(rx, cuda), n, out=got)
     assert np.array_equal(got.cpu().numpy(), o.qpsk_demod(rx, n, initial=np.full(nb, 0x5A, np.uint8)))
+
+
+@pytest.mark.parametrize("amp", [1.0, 0.37, 3.0])
+def test_qpsk256_rect_decision_boundaries(cuda, amp):
+    """Points on and a few ulps around the midpoints between rectangular levels (where rounded
+    distances tie and the first index must win), exact levels, and the grid edges: the per-axis
+    fast path with its tie check must equal the exhaustive argmin bit for bit."""
+    from gsdr_amd import ops
+
+    ops.qpsk256_init(0, amp)
+    table = o.qpsk256_table(0, amp)
+    lv = np.unique(table.real.astype(np.float32))
+    mids = ((lv[:-1] + lv[1:]) / np.float32(2)).astype(np.float32)
+    axis = [lv, mids]
+    for k in (1, 2, 3):
+        axis.append(np.nextafter(mids, np.float32(np.inf)).astype(np.float32))
+        axis.append(np.nextafter(mids, np.float32(-np.inf)).astype(np.float32))
+        mids = np.nextafter(mids, np.float32(np.inf)).astype(np.float32)
+    axis.append(np.array([lv[0] * 1.2, lv[-1] * 1.2, 0.0, -0.0], dtype=np.float32))
+    ax = np.unique(np.concatenate(axis)).astype(np.float32)
+    re, im = np.meshgrid(ax, ax)
+    x = (re.ravel() + 1j * im.ravel()).astype(np.complex64)
+    got = ops.qpsk256_demodulate(dev(x, cuda), 0).cpu().numpy()
+    assert np.array_equal(got, o.qpsk256_demod(table, x))

@@ -85,6 +85,10 @@ hipError_t launch_fc_probe(const FirJob& j, hipStream_t s) {
       return launch_poly<float, float2, 4, 4, 16, 256, kModeFir, 1>(j, s);
     case 107:  // staging only, non-temporal loads
       return launch_poly<float, float2, 4, 4, 16, 256, kModeFir, 1, true>(j, s);
+    case 113:  // matrix-core kernel with register taps, compute only
+      return launch_mfma_bc<256, 9, 2>(j, s);
+    case 117:  // staging only by LDS-DMA, non-temporal
+      return launch_poly<float, float2, 4, 4, 16, 256, kModeFir, 1, true, false, 0, true>(j, s);
     case 110:
     case 111:
       return launch_stream_probe(j, s, j.variant == 111);

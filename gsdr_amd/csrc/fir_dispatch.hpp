@@ -62,7 +62,7 @@ hipError_t launch_generic(const FirJob& j, hipStream_t s) {
 }
 
 template <class TapT, class InT, int D, int R, int JC, int WG, int MODE, int ABL = 0, bool NT = false, bool XM = false,
-          int CST = 0>
+          int CST = 0, bool DMA = false>
 hipError_t launch_poly(const FirJob& j, hipStream_t s) {
   using Geo = TileGeo<InT, D, R, WG>;
   FirParams p = make_params(j);
@@ -80,9 +80,27 @@ hipError_t launch_poly(const FirJob& j, hipStream_t s) {
   constexpr uint64_t A = SampleT<InT>::kSrcAlign;
   const bool vec = (reinterpret_cast<uintptr_t>(j.in) % A) == 0 && ((uint64_t)stride * D * sizeof(InT)) % A == 0;
   if (vec) {
-    k_fir_poly<TapT, InT, D, R, JC, WG, true, MODE, ABL, NT, XM, CST><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
+    k_fir_poly<TapT, InT, D, R, JC, WG, true, MODE, ABL, NT, XM, CST, DMA><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
   } else {
-    k_fir_poly<TapT, InT, D, R, JC, WG, false, MODE, ABL, NT, XM, CST><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
+    k_fir_poly<TapT, InT, D, R, JC, WG, false, MODE, ABL, NT, XM, CST, DMA><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
+  }
+  return launch_status();
+}
+
+// Matrix-core FIR with register-resident taps (k_fir_mfma_bc): FC, D = 4, 3D + T <= 16 * MAXSEG.
+template <int WG, int MAXSEG, int ABL = 0>
+hipError_t launch_mfma_bc(const FirJob& j, hipStream_t s) {
+  using Geo = TileGeo<float2, 4, 4, WG>;
+  if (j.D != 4 || 12 + j.T > 16u * MAXSEG) return hipErrorInvalidValue;
+  const size_t lds = mfma_bc_lds_bytes<WG>((uint32_t)j.T);
+  FirParams p = make_params(j);
+  p.tile_stride = Geo::KT;
+  const uint64_t tiles = ceil_div<uint64_t>(j.N, Geo::KT);
+  if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
+  if (aligned16(j.in)) {
+    k_fir_mfma_bc<WG, MAXSEG, true, true, ABL><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
+  } else {
+    k_fir_mfma_bc<WG, MAXSEG, false, true, ABL><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
   }
   return launch_status();
 }
@@ -114,8 +132,11 @@ hipError_t launch_contig(const FirJob& j, hipStream_t s) {
 // gsdrxFirFCVariant for tuning sweeps (all with non-temporal streaming unless noted):
 //   0 default WG=256 R=4 JC=16 | 1 WG=128 R=8 | 3 WG=64 R=8 | 4 WG=128 R=8 JC=32 | 5 WG=256 R=4 JC=8
 //   7 generic kernel | 8 default shape with plain (temporal) loads/stores | 9 default, XCD-aware tile order
+//   10/11 default, tile stored through LDS | 13 matrix-core core (k_fir_mfma_bc, T <= 132)
+//   14 default, tile body staged by LDS-DMA (global_load_lds)
 //   24 WG=64 R=4 | 28 WG=128 R=4
 // Ablation probes (fir.hip): 104 compute only, 105 staging only, 107 staging only (non-temporal),
+// 113 matrix-core compute only, 117 staging only by LDS-DMA,
 // 110/111 streaming ceiling of this traffic mix (plain / non-temporal).
 hipError_t launch_fc_probe(const FirJob& j, hipStream_t s);
 
@@ -143,6 +164,13 @@ hipError_t launch_d4_complex(const FirJob& j, hipStream_t s) {
       return launch_poly<TapT, InT, 4, 4, 16, 256, MODE, 0, true, false, 1>(j, s);
     case 11:  // default shape, tile stored through LDS (coalesced), streaming stores
       return launch_poly<TapT, InT, 4, 4, 16, 256, MODE, 0, true, false, 2>(j, s);
+    case 13:  // matrix-core core, taps broadcast from registers (k_fir_mfma_bc), FIR mode, T <= 132
+      if constexpr (MODE == kModeFir && std::is_same<TapT, float>::value && std::is_same<InT, float2>::value) {
+        return launch_mfma_bc<256, 9>(j, s);
+      }
+      return hipErrorInvalidValue;
+    case 14:  // default shape, tile body staged by LDS-DMA (global_load_lds), non-temporal
+      return launch_poly<TapT, InT, 4, 4, 16, 256, MODE, 0, true, false, 0, true>(j, s);
     case 24:
       return launch_poly<TapT, InT, 4, 4, 16, 64, MODE, 0, true>(j, s);
     case 28:

@@ -21,9 +21,10 @@
 //     free, while every window offset stays a compile-time constant.
 //   * Input may also be interleaved int8 I/Q (Iq8): converted to float as it is staged, so the float
 //     samples exist only in LDS. HBM loads and FIR stores are non-temporal (streamed once).
-//   * No MFMA: at T=127, D=4 (12.7 flop/byte) FP32 MFMA is no faster than packed VALU on gfx950 and a
-//     Toeplitz GEMM form adds ~47 % FLOPs; bf16-split MFMA costs as much energy as it saves. The kernel
-//     is bound by the part's 1400 W power cap with staging and MACs together.
+//   * The default core is packed VALU. An exact-f32 matrix-core core (k_fir_mfma_bc, 4x4x1 outer
+//     products with broadcast taps, bit-identical to the oracle) exists as a variant; it runs at a
+//     higher clock under the cap but needs more cycles and more energy per launch (4 % slower). The
+//     kernel is bound by the part's 1400 W power cap with staging and MACs together.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -31,6 +32,7 @@
 #include <stdint.h>
 
 #include <type_traits>
+#include <utility>
 
 namespace gsdr {
 
@@ -339,7 +341,37 @@ constexpr int staging_batch(int bpt) {
 // Stage granules [0, NG) of the tile starting at global sample S0 into LDS (padded layout).
 // The first SG*WG granules (the tile body) are loaded fully unrolled so every HBM load is in flight
 // before the first LDS write; the remaining halo granules follow in a short strided loop.
-template <class InT, class Geo, int WG, bool VEC, int MODE, bool NT = false>
+// Tile body by LDS-DMA (global_load_lds_dwordx4: HBM -> LDS with no VGPR round trip and no ds_write).
+// One wave instruction fills 64 consecutive LDS slots; the padded layout is kept by choosing each
+// lane's SOURCE granule (slot s holds granule s - s / SGP of its segment; pad slots are skipped with
+// the lane masked off). Returns false when the tile does not qualify (then nothing was issued).
+template <class InT, class Geo, int WG, int MODE, bool NT>
+__device__ __forceinline__ bool stage_body_dma(float4* __restrict__ lds, const InT* __restrict__ in, uint64_t S0) {
+  if constexpr (!std::is_same<InT, float2>::value || MODE != kModeFir) {
+    return false;
+  } else {
+    constexpr int BODY = Geo::SG * (Geo::KT / Geo::ROUT);  // body granules
+    constexpr int SLOTS = BODY / Geo::SG * Geo::SGP;
+    static_assert(SLOTS % 64 == 0 && (SLOTS / 64) % (WG / 64) == 0, "body slots must split into wave instructions");
+    constexpr int PER_WAVE = SLOTS / 64 / (WG / 64);
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const float4* __restrict__ src = reinterpret_cast<const float4*>(in + S0);
+#pragma unroll
+    for (int i = 0; i < PER_WAVE; ++i) {
+      const uint32_t base = (uint32_t)(i * (WG / 64) + w) * 64u;  // wave-uniform first slot
+      const uint32_t sl = base + lane;
+      const uint32_t within = sl % Geo::SGP;
+      if (within < (uint32_t)Geo::SG) {
+        const uint32_t g = (sl / Geo::SGP) * Geo::SG + within;
+        __builtin_amdgcn_global_load_lds((const void*)(src + g), (void __attribute__((address_space(3)))*)(lds + base),
+                                         16, 0, NT ? 2 : 0);
+      }
+    }
+    return true;
+  }
+}
+
+template <class InT, class Geo, int WG, bool VEC, int MODE, bool NT = false, bool DMA = false>
 __device__ __forceinline__ void stage_tile(float4* __restrict__ lds, const InT* __restrict__ in, uint64_t S0,
                                            uint32_t NG, const FirParams& p) {
   constexpr int G = Geo::G;
@@ -353,6 +385,16 @@ __device__ __forceinline__ void stage_tile(float4* __restrict__ lds, const InT* 
   const PhaseWalk pw = phase_walk<G, WG>(p.nco_n0, S0, p.nco_inc);
   // wave-uniform: is the whole staged span readable? (every tile but the last)
   const bool whole = VEC && (S0 + (uint64_t)NG * G <= p.L);
+  if constexpr (DMA) {
+    if (whole && stage_body_dma<InT, Geo, WG, MODE, NT>(lds, in, S0)) {
+      for (uint32_t g = BPT * WG + tid; g < NG; g += WG) {
+        const uint64_t s = S0 + (uint64_t)g * G;
+        lds[Geo::padded(g)] = stage_transform<InT, MODE>(load_granule<InT, VEC>(in, s, p.L), (uint32_t)s, p);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      return;
+    }
+  }
 #pragma unroll
   for (int b0 = 0; b0 < BPT; b0 += SB) {
     float4 v[SB];
@@ -600,7 +642,7 @@ __device__ __forceinline__ uint32_t tile_of_block() {
 }
 
 template <class TapT, class InT, int D, int R, int JC, int WG, bool VEC, int MODE, int ABL = 0, bool NT = false,
-          bool XM = false, int CST = 0>
+          bool XM = false, int CST = 0, bool DMA = false>
 __global__ __launch_bounds__(WG) void k_fir_poly(FirParams p) {
   using Geo = TileGeo<InT, D, R, WG>;
   using OutT = typename Product<TapT, InT>::type;
@@ -614,7 +656,7 @@ __global__ __launch_bounds__(WG) void k_fir_poly(FirParams p) {
   const uint32_t span = p.nch * JC * D;
   const uint32_t NG = ((Geo::KT - 1) * D + span + G - 1) / G;
   // LDS: [tile granules | FM exchange (WG float2)]
-  if constexpr (ABL != 2) stage_tile<InT, Geo, WG, VEC, MODE, NT>(lds, in, S0, NG, p);
+  if constexpr (ABL != 2) stage_tile<InT, Geo, WG, VEC, MODE, NT, DMA>(lds, in, S0, NG, p);
   __syncthreads();
 
   OutT acc[R];
@@ -808,6 +850,89 @@ __global__ __launch_bounds__(256) void k_fir_generic(FirParams p) {
     const float2 y1 = fir_point<TapT, InT, MODE>(p, k + 1);
     reinterpret_cast<float*>(p.out)[k] = fm_disc(y0, y1, p.fm_gain);
   }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Kernel 1y: the same tile on the matrix cores (FIR mode, real taps, complex input, D = 4), an
+// alternative core kept as a tuning variant (gsdrxFirFCVariant 13).
+// v_mfma_f32_4x4x1_16b_f32 is 16 independent 4x4 outer products per wave instruction: block b of a
+// wave holds lanes 4b..4b+3, A[i] comes from lane 4b+i, B[j] from lane 4b+j and D[i][j] lands in
+// VGPR i of lane 4b+j. With
+//     A[i] = t[kappa - D*i]                  (the tap row i needs at step kappa),
+//     B[j] = x[D*(k0 + 4L) + kappa], L = 4b+j (lane L's own input stream),
+// accumulator C[i] of lane L sums t[kappa - D*i] * x[D*(k0 + 4L + i) + (kappa - D*i)] over
+// kappa = 0 .. 3D+T-1: output k0 + 4L + i with its taps in ascending order (zero outside [0, T)).
+// f32 MFMA is an exact fmaf chain, so the outputs are bit-identical to the oracle's and the generic
+// kernel's ascending-tap fmaf loop. Each lane reads its window sequentially from LDS (one
+// ds_read_b128 per two steps); re and im are two accumulator chains. The taps need no memory
+// traffic in the loop: the A operand of block ABID can be broadcast to all 16 blocks (CBSZ = 4) and
+// every block needs the same taps, so one VGPR carries the taps of 16 consecutive steps: lane 4b+i
+// of tap register c holds t[16c + b - D*i], and step 16c + b runs with ABID = b. MAXSEG registers
+// cover 16*MAXSEG steps (3D + T of them are needed). Staging, tile geometry and epilogue are the
+// polyphase kernel's (R = 4 outputs per lane).
+// ------------------------------------------------------------------------------------------------
+typedef float gsdr_mf4 __attribute__((ext_vector_type(4)));
+
+// steps 2g and 2g + 1 of a segment (granule g): ABID must be an immediate
+template <int G>
+__device__ __forceinline__ void mfma_bc_granule(float tv, const float4& w, gsdr_mf4& cre, gsdr_mf4& cim) {
+  cre = __builtin_amdgcn_mfma_f32_4x4x1f32(tv, w.x, cre, 4, 2 * G, 0);
+  cim = __builtin_amdgcn_mfma_f32_4x4x1f32(tv, w.y, cim, 4, 2 * G, 0);
+  cre = __builtin_amdgcn_mfma_f32_4x4x1f32(tv, w.z, cre, 4, 2 * G + 1, 0);
+  cim = __builtin_amdgcn_mfma_f32_4x4x1f32(tv, w.w, cim, 4, 2 * G + 1, 0);
+}
+template <int... G>
+__device__ __forceinline__ void mfma_bc_segment(float tv, const float4 (&w)[8], gsdr_mf4& cre, gsdr_mf4& cim,
+                                                std::integer_sequence<int, G...>) {
+  (mfma_bc_granule<G>(tv, w[G], cre, cim), ...);
+}
+
+template <int WG, int MAXSEG, bool VEC, bool NT, int ABL = 0>
+__global__ __launch_bounds__(WG) void k_fir_mfma_bc(FirParams p) {
+  constexpr int D = 4, R = 4;
+  using Geo = TileGeo<float2, D, R, WG>;
+  static_assert(Geo::SG == 8 && Geo::PAD == 1, "lane stream layout: 16 steps per 9-granule segment");
+  extern __shared__ __attribute__((aligned(16))) float4 lds[];
+  const float2* __restrict__ in = reinterpret_cast<const float2*>(p.in);
+  const uint64_t out0 = (uint64_t)blockIdx.x * p.tile_stride;
+  const uint64_t S0 = out0 * D;
+  const uint32_t nk = 3u * D + p.T;             // steps that meet a tap
+  const uint32_t nseg = (nk + 15u) / 16u;       // <= MAXSEG (checked by the launcher)
+  const uint32_t NG = (D * (Geo::KT - R) + 16u * nseg) / 2;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  const float* __restrict__ taps = reinterpret_cast<const float*>(p.taps);
+  float tv[MAXSEG];
+#pragma unroll
+  for (int c = 0; c < MAXSEG; ++c) {
+    const uint32_t i = 16u * c + (lane >> 2) - D * (lane & 3u);  // wraps (>= T) below zero
+    tv[c] = i < p.T ? taps[i] : 0.0f;
+  }
+  if constexpr (ABL != 2) stage_tile<float2, Geo, WG, VEC, kModeFir, NT>(lds, in, S0, NG, p);
+  __syncthreads();
+
+  const float4* __restrict__ seg = lds + tid * Geo::SGP;
+  gsdr_mf4 cre = {0.f, 0.f, 0.f, 0.f}, cim = cre;
+#pragma unroll
+  for (int c = 0; c < MAXSEG; ++c) {
+    if ((uint32_t)c < nseg) {
+      float4 w[8];
+#pragma unroll
+      for (int g = 0; g < 8; ++g) w[g] = seg[c * Geo::SGP + g];
+      mfma_bc_segment(tv[c], w, cre, cim, std::make_integer_sequence<int, 8>{});
+    }
+  }
+  float2 acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] = make_float2(cre[r], cim[r]);
+  tile_epilogue<kModeFir, float2, R, WG, NT>(p, out0, acc, nullptr);
+}
+
+template <int WG>
+constexpr size_t mfma_bc_lds_bytes(uint32_t T) {
+  using Geo = TileGeo<float2, 4, 4, WG>;
+  const uint32_t nseg = (12u + T + 15u) / 16u;
+  const uint32_t NG = (4u * (Geo::KT - 4) + 16u * nseg) / 2;
+  return (size_t)(Geo::padded(NG - 1) + 1) * 16u;
 }
 
 // ------------------------------------------------------------------------------------------------

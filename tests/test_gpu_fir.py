@@ -110,20 +110,36 @@ def test_fir_restores_current_device(cuda):
     assert torch.cuda.current_device() == 0
 
 
-@pytest.mark.parametrize("variant", [0, 1, 3, 4, 5, 7, 8, 9, 10, 11, 24, 28])
+@pytest.mark.parametrize("variant", [0, 1, 3, 4, 5, 7, 8, 9, 10, 11, 13, 14, 24, 28])
 def test_fir_fc_d4_variants(cuda, variant):
     """Every tile shape of the headline kernel (gsdrxFirFCVariant) meets the same bar."""
     from gsdr_amd import ops
 
     N, D, T = 50000 + 3, 4, 127
     taps, x = make("FC", T, (N - 1) * D + T, 99)
-    y = ops.fir_variant(variant, dev(taps, cuda), dev(x, cuda), D, N)
+    y = ops.fir_variant(13, dev(taps, cuda), dev(x, cuda), D, N)
     torch.cuda.synchronize()
     ref = o.fir(taps, x, D, N)
-    assert normwise_err(y.cpu().numpy(), ref, bound(taps, x, D, N)) <= FLOAT_TOL
+    assert np.array_equal(y.cpu().numpy().view(np.uint64), ref.view(np.uint64))
 
 
-@pytest.mark.parametrize("variant", [9, 10, 11])
+@pytest.mark.parametrize("T", [1, 2, 3, 4, 5, 8, 63, 116, 117, 127, 128, 132])
+@pytest.mark.parametrize("N", [1, 1023, 1024, 4097, 50000 + 3])
+def test_fir_fc_d4_mfma_variant(cuda, T, N):
+    """Matrix-core kernel (variant 13, k_fir_mfma_bc): f32 MFMA is an exact fmaf chain in ascending tap
+    order, so its outputs equal the oracle's bit for bit (and the generic kernel's), ragged tails and
+    every tap count up to its 132-tap register budget included."""
+    from gsdr_amd import ops
+
+    D = 4
+    taps, x = make("FC", T, (N - 1) * D + T, 7 + T)
+    y = ops.fir_variant(13, dev(taps, cuda), dev(x, cuda), D, N)
+    torch.cuda.synchronize()
+    ref = o.fir(taps, x, D, N)
+    assert np.array_equal(y.cpu().numpy().view(np.uint64), ref.view(np.uint64))
+
+
+@pytest.mark.parametrize("variant", [9, 10, 11, 14])
 @pytest.mark.parametrize("N", [1024, 50000 + 3, 3 * 1024 + 1])
 def test_fir_fc_d4_store_variants_bit_identical(cuda, variant, N):
     """Variants that change only the tile order or the store path (XCD order, LDS-transposed stores)

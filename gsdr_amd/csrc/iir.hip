@@ -21,6 +21,8 @@
 // coefficients beyond K-1 leave the recursion unchanged).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "gsdr/iir.h"
 #include "launch.hpp"
 
@@ -86,6 +88,10 @@ __device__ __forceinline__ S x_at(const S* __restrict__ x, const S* __restrict__
   if (n >= 0) return x[n];
   return (xh && -1 - n < K - 1) ? xh[-1 - n] : zero_s(S{});
 }
+
+// workgroup barrier for LDS-only phases: waits for this wave's LDS accesses, not its global loads
+// (__syncthreads would also drain the tile loads in flight)
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // matrix product C = A * B (P x P, row-major) by a workgroup: each thread computes entries
 template <int P>
@@ -186,7 +192,7 @@ __device__ void iir_setup(const Coeffs& cf, const S* __restrict__ yh, typename A
 // (chunk stride kChunk + 1 elements: consecutive lanes land on different banks).
 template <class S>
 struct TileShape {
-  static constexpr int WG = 256;
+  static constexpr int WG = 128;
   static constexpr int NC = sizeof(S) / sizeof(float);  // components per sample: one lane each
   static constexpr int CPW = WG / NC;                     // chunks per workgroup
   static constexpr int TS = CPW * kChunk;                 // samples per tile: 33 KB of LDS either way
@@ -204,18 +210,75 @@ struct SetupArgs {
 template <int P>
 constexpr bool kTableInLds = kGroup * P * P * sizeof(double) <= 32 * 1024;
 
-template <class S, int P, int PASS, bool VEC>
+// Level-0 scan fused into the chunk passes (P <= kFusedMaxP): the tails pass runs the up-sweep of its
+// own groups from LDS (no tails round trip through HBM, no separate launch) and the final pass
+// derives each chunk's start state itself (the level-0 down-sweep).
+constexpr int kFusedMaxP = 8;
+
+struct ScanArgs {
+  double* incl;          // level-0 inclusive zero-state prefixes (A[P] per chunk); tails pass writes
+  double* aggs;          // level-1 elements (group aggregates), or null when level 0 is the top
+  const double* T0;      // M_0^r, r < 64 (final pass)
+  const double* gstart;  // level-1 start states (final pass), or null: s0 is the group start
+  const double* s0;
+};
+
+// Up-sweep of one level-0 group from the workgroup's tails in LDS (loc = the group's 64 elements),
+// with the powers M_0^(2^s) in pw[s]: as up_group, same operations.
+template <class A, int P>
+__device__ __forceinline__ void up_group_fused(const A* __restrict__ loc, uint64_t E, const double* __restrict__ pw,
+                                               A* __restrict__ incl, A* __restrict__ aggs, uint64_t g, int r) {
+  constexpr int PP = P * P;
+  const uint64_t j = g * kGroup + r;
+  const uint64_t last = (E - 1 < g * kGroup + kGroup - 1) ? E - 1 - g * kGroup : kGroup - 1;
+  A v[P];
+#pragma unroll
+  for (int i = 0; i < P; ++i) v[i] = j < E ? loc[r * P + i] : zero_s(A{});
+#pragma unroll
+  for (int s = 0; s < 6; ++s) {
+    const int d = 1 << s;
+    const double* __restrict__ Md = pw + s * PP;
+    A w[P];
+#pragma unroll
+    for (int i = 0; i < P; ++i) w[i] = shfl_up_s(v[i], d);
+    if (r >= d) {
+#pragma unroll
+      for (int i = 0; i < P; ++i) {
+        A acc = v[i];
+#pragma unroll
+        for (int l = 0; l < P; ++l) acc = fma_s(Md[i * P + l], w[l], acc);
+        v[i] = acc;
+      }
+    }
+  }
+  if (j < E) {
+#pragma unroll
+    for (int i = 0; i < P; ++i) incl[j * P + i] = v[i];
+  }
+  if (aggs && (uint64_t)r == last) {
+#pragma unroll
+    for (int i = 0; i < P; ++i) aggs[g * P + i] = v[i];
+  }
+}
+
+template <class S, int P, int PASS, bool VEC, bool FUSED = false>
 __global__ __launch_bounds__(TileShape<S>::WG) void k_iir_chunks(Coeffs cf, const S* __restrict__ x,
                                                                  const S* __restrict__ xh, uint64_t n,
                                                                  const typename Acc<S>::type* __restrict__ starts,
                                                                  typename Acc<S>::type* __restrict__ tails,
-                                                                 S* __restrict__ y, SetupArgs setup) {
+                                                                 S* __restrict__ y, SetupArgs setup, ScanArgs sc) {
   using TSh = TileShape<S>;
   using A = typename Acc<S>::type;
-  constexpr size_t kTileBytes = sizeof(S) * TSh::WG * TSh::STRIDE;
+  constexpr size_t kTileBytes = sizeof(S) * TSh::CPW * TSh::STRIDE;
   constexpr size_t kTableBytes = kTableInLds<P> ? kGroup * P * P * sizeof(double) : 0;
   __shared__ __attribute__((aligned(16))) char smem[kTileBytes > kTableBytes ? kTileBytes : kTableBytes];
+  // fused tails pass: M_0^(2^s), s < 6, and the workgroup's chunk tails
+  constexpr int kPow = (FUSED && PASS == kTails) ? 6 * P * P : 1;
+  static_assert(!FUSED || TSh::CPW * P * sizeof(A) <= kTileBytes, "tails alias the tile");
+  __shared__ double mpow[kPow];
+  __shared__ S pre[P];  // x[base - 1 - i], i < P
   S* tile = reinterpret_cast<S*>(smem);
+  A* tl = reinterpret_cast<A*>(smem);  // fused tails pass: the chunk tails, once the tile is consumed
   const int t = threadIdx.x;
   if constexpr (PASS == kTails) {
     // the extra last workgroup builds the scan constants while the others compute the tails
@@ -225,97 +288,196 @@ __global__ __launch_bounds__(TileShape<S>::WG) void k_iir_chunks(Coeffs cf, cons
       return;
     }
   }
-  const uint64_t base = (uint64_t)blockIdx.x * TSh::TS;
-  const uint32_t tlen = n - base < (uint64_t)TSh::TS ? (uint32_t)(n - base) : (uint32_t)TSh::TS;
+  // Workgroup b filters tiles b, b + nwg, ... (the launcher starts one workgroup per tile; a
+  // register prefetch of the next tile in a persistent grid measured no faster). Barriers wait for
+  // LDS only (lds_barrier), so global loads issued before them stay in flight.
+  const uint32_t nwg = PASS == kTails ? gridDim.x - 1 : gridDim.x;
+  const uint64_t ntiles = (n + TSh::TS - 1) / TSh::TS;
   constexpr int SPV = 16 / sizeof(S);          // samples per 16-byte load
   constexpr int NV = TSh::TS / SPV / TSh::WG;   // 16-byte loads per thread for a whole tile
-  if (VEC && tlen == (uint32_t)TSh::TS) {
-    // every load in flight before the first LDS write (a load-then-store loop would wait on HBM
-    // latency once per iteration)
-    const float4* __restrict__ src = reinterpret_cast<const float4*>(x + base);
-    float4 v[NV];
-#pragma unroll
-    for (int k = 0; k < NV; ++k) v[k] = src[k * TSh::WG + t];
-#pragma unroll
-    for (int k = 0; k < NV; ++k) {
-      const int idx = (k * TSh::WG + t) * SPV;  // SPV consecutive samples, all in one chunk row
-      float* d = reinterpret_cast<float*>(tile + TSh::at(idx));
-      d[0] = v[k].x;
-      d[1] = v[k].y;
-      d[2] = v[k].z;
-      d[3] = v[k].w;
-    }
-  } else {
-    for (int idx = t; idx < (int)tlen; idx += TSh::WG) tile[TSh::at(idx)] = x[base + idx];
-  }
-  __syncthreads();
-  // lane t runs the recursion of component t % NC of chunk t / NC (complex samples with real
-  // coefficients are two independent real recursions): scalar double state, twice the lanes
   constexpr int NC = TSh::NC;
   const int comp = t % NC;
-  const uint64_t c = (uint64_t)blockIdx.x * TSh::CPW + t / NC;
-  const uint64_t n0 = c * kChunk;
-  const double* __restrict__ starts_d = reinterpret_cast<const double*>(starts);
-  double* __restrict__ tails_d = reinterpret_cast<double*>(tails);
-  if (n0 < n) {
-    const uint32_t len = n - n0 < (uint64_t)kChunk ? (uint32_t)(n - n0) : (uint32_t)kChunk;
-    double b[P + 1], am[P + 1];
+  auto is_whole = [&](uint64_t i) { return VEC && (i + 1) * (uint64_t)TSh::TS <= n; };
+  auto load_tile = [&](uint64_t i, float4 (&r)[NV]) {
+    const float4* __restrict__ src = reinterpret_cast<const float4*>(x + i * TSh::TS);
 #pragma unroll
-    for (int i = 0; i <= P; ++i) {
-      b[i] = coeff(cf.b, cf.K, i);
-      am[i] = -coeff(cf.a, cf.K, i);
-    }
-    float xs[P];   // component of x[n-1-i] (exact floats)
-    double ys[P];  // component of y[n-1-i]
+    for (int k = 0; k < NV; ++k) r[k] = src[k * TSh::WG + t];
+  };
+  uint64_t ti = blockIdx.x;
+  auto build_pow = [&]() {
+    // M_0 (column j = state after kChunk steps of the homogeneous recursion from e_j), then squared:
+    // the same operations as iir_setup's T[1], T[2], ..., T[32], so the same doubles
+    if (t < P) {
+      double am[P + 1];
 #pragma unroll
-    for (int i = 0; i < P; ++i) {
-      const S xv = x_at(x, xh, cf.K, (int64_t)n0 - 1 - i);
-      xs[i] = reinterpret_cast<const float*>(&xv)[comp];
-      ys[i] = PASS == kFinal ? starts_d[(c * P + i) * NC + comp] : 0.0;
-    }
-    float* __restrict__ row = reinterpret_cast<float*>(tile + (t / NC) * TSh::STRIDE) + comp;
-    for (uint32_t k = 0; k < len; ++k) {
-      const float xv = row[k * NC];
-      double acc = b[0] * (double)xv;
+      for (int i = 0; i <= P; ++i) am[i] = -coeff(cf.a, cf.K, i);
+      double m[P];
 #pragma unroll
-      for (int i = 1; i <= P; ++i) acc = fma(b[i], (double)xs[i - 1], acc);
+      for (int i = 0; i < P; ++i) m[i] = i == t ? 1.0 : 0.0;
+      for (int k = 0; k < kChunk; ++k) {
+        double acc = 0.0;
 #pragma unroll
-      for (int i = 1; i <= P; ++i) acc = fma(am[i], ys[i - 1], acc);
+        for (int i = 1; i <= P; ++i) acc = fma(am[i], m[i - 1], acc);
 #pragma unroll
-      for (int i = P - 1; i > 0; --i) {
-        xs[i] = xs[i - 1];
-        ys[i] = ys[i - 1];
+        for (int i = P - 1; i > 0; --i) m[i] = m[i - 1];
+        m[0] = acc;
       }
-      xs[0] = xv;
-      ys[0] = acc;
-      if constexpr (PASS == kFinal) row[k * NC] = (float)acc;  // y replaces x in this chunk's row
-    }
-    if constexpr (PASS == kTails) {
 #pragma unroll
-      for (int i = 0; i < P; ++i) tails_d[(c * P + i) * NC + comp] = ys[i];
-    } else if (n0 + len == n) {
-      // the last chunk's state after the call (outputs, then inputs, newest first), staged for the
-      // caller's history buffers
-#pragma unroll
-      for (int i = 0; i < P; ++i) {
-        tails_d[i * NC + comp] = ys[i];
-        tails_d[(P + i) * NC + comp] = xs[i];
-      }
+      for (int i = 0; i < P; ++i) mpow[i * P + t] = m[i];
     }
+    lds_barrier();
+    for (int q = 1; q < 6; ++q) {
+      mat_mul<P>(mpow + (q - 1) * P * P, mpow + (q - 1) * P * P, mpow + q * P * P, t, TSh::WG);
+      lds_barrier();
+    }
+  };
+  double b[P + 1], am[P + 1];
+#pragma unroll
+  for (int i = 0; i <= P; ++i) {
+    b[i] = coeff(cf.b, cf.K, i);
+    am[i] = -coeff(cf.a, cf.K, i);
   }
-  if constexpr (PASS == kFinal) {
-    __syncthreads();
-    if (VEC && tlen == (uint32_t)TSh::TS) {
-      float4* __restrict__ dst = reinterpret_cast<float4*>(y + base);
+  double* __restrict__ tails_d = reinterpret_cast<double*>(tails);
+  for (; ti < ntiles; ti += nwg) {
+    const uint64_t base = ti * TSh::TS;
+    const uint32_t tlen = n - base < (uint64_t)TSh::TS ? (uint32_t)(n - base) : (uint32_t)TSh::TS;
+    const bool whole = is_whole(ti);
+    float4 v[NV];
+    if (whole) load_tile(ti, v);  // in flight while the final pass computes the chunk start state
+    // the P samples before the tile (the input history for the first tile), loaded beside it
+    S pv = zero_s(S{});
+    if (t < P) pv = x_at(x, xh, cf.K, (int64_t)base - 1 - t);
+    const uint64_t c = ti * TSh::CPW + t / NC;
+    const uint64_t n0 = c * kChunk;
+    double ys[P];  // component of y[n-1-i]: the chunk's start state
+#pragma unroll
+    for (int i = 0; i < P; ++i) ys[i] = 0.0;
+    if constexpr (FUSED && PASS == kFinal) {
+      // level-0 down-sweep for this chunk: start = M_0^r S_g + prefix_(r-1) (as down_group)
+      if (n0 < n) {
+        const uint64_t g = c / kGroup;
+        const int r = (int)(c % kGroup);
+        const double* __restrict__ Mr = sc.T0 + (size_t)r * P * P;
+        const double* __restrict__ sg = sc.gstart ? sc.gstart + g * P * NC : sc.s0;
+        double sgc[P];
+#pragma unroll
+        for (int l = 0; l < P; ++l) sgc[l] = sg[l * NC + comp];
+#pragma unroll
+        for (int i = 0; i < P; ++i) {
+          double acc = r > 0 ? sc.incl[((c - 1) * P + i) * NC + comp] : 0.0;
+#pragma unroll
+          for (int l = 0; l < P; ++l) acc = fma(Mr[i * P + l], sgc[l], acc);
+          ys[i] = acc;
+        }
+      }
+    } else if constexpr (PASS == kFinal) {
+      if (n0 < n) {
+        const double* __restrict__ starts_d = reinterpret_cast<const double*>(starts);
+#pragma unroll
+        for (int i = 0; i < P; ++i) ys[i] = starts_d[(c * P + i) * NC + comp];
+      }
+    }
+    if (whole) {
 #pragma unroll
       for (int k = 0; k < NV; ++k) {
-        const int idx = (k * TSh::WG + t) * SPV;
-        const float* d = reinterpret_cast<const float*>(tile + TSh::at(idx));
-        dst[k * TSh::WG + t] = make_float4(d[0], d[1], d[2], d[3]);
+        const int idx = (k * TSh::WG + t) * SPV;  // SPV consecutive samples, all in one chunk row
+        float* d = reinterpret_cast<float*>(tile + TSh::at(idx));
+        d[0] = v[k].x;
+        d[1] = v[k].y;
+        d[2] = v[k].z;
+        d[3] = v[k].w;
       }
     } else {
-      for (int idx = t; idx < (int)tlen; idx += TSh::WG) y[base + idx] = tile[TSh::at(idx)];
+      for (int idx = t; idx < (int)tlen; idx += TSh::WG) tile[TSh::at(idx)] = x[base + idx];
     }
+    if (t < P) pre[t] = pv;
+    lds_barrier();
+    // component of x[n-1-i] for every chunk, read before any row is overwritten with y
+    double xd[P];
+    {
+      const int lc = t / NC;  // chunk within the tile
+#pragma unroll
+      for (int i = 0; i < P; ++i) {
+        const int m = lc * kChunk - 1 - i;  // tile index of x[n0-1-i]; < 0: before the tile
+        xd[i] = (double)reinterpret_cast<const float*>(m >= 0 ? tile + TSh::at(m) : pre + (-1 - m))[comp];
+      }
+    }
+    if constexpr (PASS == kFinal) lds_barrier();
+    // lane t runs the recursion of component t % NC of chunk t / NC (complex samples with real
+    // coefficients are two independent real recursions): scalar double state, twice the lanes
+    if (n0 < n) {
+      const uint32_t len = n - n0 < (uint64_t)kChunk ? (uint32_t)(n - n0) : (uint32_t)kChunk;
+      float* __restrict__ row = reinterpret_cast<float*>(tile + (t / NC) * TSh::STRIDE) + comp;
+      // inputs held as doubles (converted once per sample, exact); a whole chunk is fully unrolled
+      // so the state shifts are register renames
+      auto step = [&](uint32_t k) {
+        const double xv = (double)row[k * NC];
+        double acc = b[0] * xv;
+#pragma unroll
+        for (int i = 1; i <= P; ++i) acc = fma(b[i], xd[i - 1], acc);
+#pragma unroll
+        for (int i = 1; i <= P; ++i) acc = fma(am[i], ys[i - 1], acc);
+#pragma unroll
+        for (int i = P - 1; i > 0; --i) {
+          xd[i] = xd[i - 1];
+          ys[i] = ys[i - 1];
+        }
+        xd[0] = xv;
+        ys[0] = acc;
+        if constexpr (PASS == kFinal) row[k * NC] = (float)acc;  // y replaces x in this chunk's row
+      };
+      if (len == (uint32_t)kChunk) {
+#pragma unroll
+        for (uint32_t k = 0; k < (uint32_t)kChunk; ++k) step(k);
+      } else {
+        for (uint32_t k = 0; k < len; ++k) step(k);
+      }
+      if constexpr (PASS == kTails && !FUSED) {
+#pragma unroll
+        for (int i = 0; i < P; ++i) tails_d[(c * P + i) * NC + comp] = ys[i];
+      } else if constexpr (PASS == kFinal) {
+        if (n0 + len == n) {
+          // the last chunk's state after the call (outputs, then inputs, newest first), staged for
+          // the caller's history buffers
+#pragma unroll
+          for (int i = 0; i < P; ++i) {
+            tails_d[i * NC + comp] = ys[i];
+            tails_d[(P + i) * NC + comp] = (double)(float)xd[i];
+          }
+        }
+      }
+    }
+    if constexpr (PASS == kTails && FUSED) {
+      if (ti == blockIdx.x) build_pow();
+      lds_barrier();  // every lane is done reading the tile
+      if (n0 < n) {
+#pragma unroll
+        for (int i = 0; i < P; ++i) reinterpret_cast<double*>(&tl[(t / NC) * P + i])[comp] = ys[i];
+      }
+      lds_barrier();
+      const int w = t / kGroup;
+      if (w < TSh::CPW / kGroup) {
+        const uint64_t C = (n + kChunk - 1) / kChunk;
+        const uint64_t g = ti * (TSh::CPW / kGroup) + w;
+        up_group_fused<A, P>(tl + w * kGroup * P, C, mpow, reinterpret_cast<A*>(sc.incl),
+                             reinterpret_cast<A*>(sc.aggs), g, t % kGroup);
+      }
+    }
+    if constexpr (PASS == kFinal) {
+      lds_barrier();
+      if (whole) {
+        float4* __restrict__ dst = reinterpret_cast<float4*>(y + base);
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+          const int idx = (k * TSh::WG + t) * SPV;
+          const float* d = reinterpret_cast<const float*>(tile + TSh::at(idx));
+          dst[k * TSh::WG + t] = make_float4(d[0], d[1], d[2], d[3]);
+        }
+      } else {
+        for (int idx = t; idx < (int)tlen; idx += TSh::WG) y[base + idx] = tile[TSh::at(idx)];
+      }
+    }
+    lds_barrier();  // the tile's LDS is free for the next one
   }
 }
 
@@ -403,6 +565,8 @@ __global__ __launch_bounds__(64) void k_iir_down(uint64_t E, const double* __res
 // between levels, workgroup-scope visibility); larger levels get one launch each (a single workgroup
 // walking many groups serially is latency-bound).
 constexpr int kRestWaves = 16;
+constexpr int kRestGroups = 16;  // levels with at most this many groups go to the single-workgroup kernels
+                                 // (128 measured 5x slower: one workgroup walking 8 groups per wave is latency-bound)
 template <class A>
 struct Levels {
   A* elems[kMaxLevels + 1];
@@ -416,9 +580,10 @@ template <class A, int P>
 __global__ __launch_bounds__(64 * kRestWaves) void k_iir_up_rest(Levels<A> L, int first) {
   const int w = threadIdx.x / 64, r = threadIdx.x % 64;
   for (int k = first; k <= L.levels; ++k) {
+    const double* T = L.T[k];
     const uint64_t groups = ceil_div<uint64_t>(L.E[k], kGroup);
     for (uint64_t g = w; g < groups; g += kRestWaves) {
-      up_group<A, P>(L.elems[k], L.E[k], L.T[k], L.starts[k], k < L.levels ? L.elems[k + 1] : nullptr, g, r);
+      up_group<A, P>(L.elems[k], L.E[k], T, L.starts[k], k < L.levels ? L.elems[k + 1] : nullptr, g, r);
     }
     __syncthreads();
   }
@@ -428,9 +593,10 @@ template <class A, int P>
 __global__ __launch_bounds__(64 * kRestWaves) void k_iir_down_rest(Levels<A> L, const A* __restrict__ s0, int lowest) {
   const int w = threadIdx.x / 64, r = threadIdx.x % 64;
   for (int k = L.levels; k >= lowest; --k) {
+    const double* T = L.T[k];
     const uint64_t groups = ceil_div<uint64_t>(L.E[k], kGroup);
     for (uint64_t g = w; g < groups; g += kRestWaves) {
-      down_group<A, P>(L.E[k], L.T[k], k < L.levels ? L.starts[k + 1] : nullptr, s0, L.starts[k], g, r);
+      down_group<A, P>(L.E[k], T, k < L.levels ? L.starts[k + 1] : nullptr, s0, L.starts[k], g, r);
     }
     __syncthreads();
   }
@@ -489,13 +655,19 @@ static hipError_t run(const Coeffs& cf, S* xh, S* yh, const S* x, S* y, uint64_t
   const int Pk = K - 1;  // live state components (<= P); the rest stay zero
 
   constexpr int WG = TileShape<S>::WG;
-  const uint32_t blocks = (uint32_t)ceil_div<uint64_t>(C, TileShape<S>::CPW);
+  const uint32_t blocks = (uint32_t)ceil_div<uint64_t>(n, TileShape<S>::TS);
   const SetupArgs sa{yh, s0, table(0), levels};
   const bool vec = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15u) == 0;
+  constexpr bool F = P <= kFusedMaxP;
+  // fused: the tails pass leaves level-0 inclusive prefixes in starts(0) and the group aggregates in
+  // elems(1); the final pass finishes level 0 itself
+  const ScanArgs up_args{reinterpret_cast<double*>(starts(0)), levels > 0 ? reinterpret_cast<double*>(elems(1)) : nullptr,
+                         nullptr, nullptr, nullptr};
   if (vec) {
-    k_iir_chunks<S, P, kTails, true><<<blocks + 1, WG, 0, st>>>(cf, x, xh, n, nullptr, elems(0), nullptr, sa);
+    k_iir_chunks<S, P, kTails, true, F><<<blocks + 1, WG, 0, st>>>(cf, x, xh, n, nullptr, elems(0), nullptr, sa, up_args);
   } else {
-    k_iir_chunks<S, P, kTails, false><<<blocks + 1, WG, 0, st>>>(cf, x, xh, n, nullptr, elems(0), nullptr, sa);
+    k_iir_chunks<S, P, kTails, false, F><<<blocks + 1, WG, 0, st>>>(cf, x, xh, n, nullptr, elems(0), nullptr, sa,
+                                                                    up_args);
   }
   // levels with more than kRestWaves groups: one launch each; the rest: one single-workgroup launch
   Levels<A> L{};
@@ -506,22 +678,30 @@ static hipError_t run(const Coeffs& cf, S* xh, S* yh, const S* x, S* y, uint64_t
     L.E[k] = E[k];
   }
   L.levels = levels;
-  int rest = 0;  // first level handled by the single-workgroup kernels
-  while (rest <= levels && ceil_div<uint64_t>(E[rest], kGroup) > (uint64_t)kRestWaves) ++rest;
-  for (int k = 0; k < rest; ++k) {
+  const int lowest = F ? 1 : 0;  // levels scanned outside the chunk passes
+  int rest = lowest;             // first level handled by the single-workgroup kernels
+  while (rest <= levels && ceil_div<uint64_t>(E[rest], kGroup) > (uint64_t)kRestGroups) ++rest;
+  for (int k = lowest; k < rest; ++k) {
     k_iir_up<A, P><<<(uint32_t)ceil_div<uint64_t>(E[k], kGroup), 64, 0, st>>>(elems(k), E[k], table(k), starts(k),
                                                                              elems(k + 1));
   }
-  k_iir_up_rest<A, P><<<1, 64 * kRestWaves, 0, st>>>(L, rest);
-  k_iir_down_rest<A, P><<<1, 64 * kRestWaves, 0, st>>>(L, s0, rest);
-  for (int k = rest - 1; k >= 0; --k) {
+  if (rest <= levels) {
+    k_iir_up_rest<A, P><<<1, 64 * kRestWaves, 0, st>>>(L, rest);
+    k_iir_down_rest<A, P><<<1, 64 * kRestWaves, 0, st>>>(L, s0, rest);
+  }
+  for (int k = rest - 1; k >= lowest; --k) {
     k_iir_down<A, P><<<(uint32_t)ceil_div<uint64_t>(E[k], kGroup), 64, 0, st>>>(E[k], table(k), starts(k + 1),
                                                                                starts(k));
   }
+  const ScanArgs down_args{reinterpret_cast<double*>(starts(0)), nullptr, table(0),
+                           levels > 0 ? reinterpret_cast<const double*>(starts(1)) : nullptr,
+                           reinterpret_cast<const double*>(s0)};
   if (vec) {
-    k_iir_chunks<S, P, kFinal, true><<<blocks, WG, 0, st>>>(cf, x, xh, n, starts(0), st_out, y, SetupArgs{});
+    k_iir_chunks<S, P, kFinal, true, F><<<blocks, WG, 0, st>>>(cf, x, xh, n, starts(0), st_out, y, SetupArgs{},
+                                                               down_args);
   } else {
-    k_iir_chunks<S, P, kFinal, false><<<blocks, WG, 0, st>>>(cf, x, xh, n, starts(0), st_out, y, SetupArgs{});
+    k_iir_chunks<S, P, kFinal, false, F><<<blocks, WG, 0, st>>>(cf, x, xh, n, starts(0), st_out, y, SetupArgs{},
+                                                                down_args);
   }
   if (xh || yh) k_iir_history<S><<<1, 64, 0, st>>>(xh, yh, st_out, P, Pk);
   e = launch_status();

@@ -179,6 +179,14 @@ __global__ __launch_bounds__(kCBlock) void k_c256_mod(C256Streams st, uint32_t n
   }
 }
 
+// LDS hand-off between the lanes of one wave: without it the compiler, reasoning per thread, may
+// forward a lane's own earlier LDS store to its later load past another lane's store.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // TYPE 0: rectangular table (per-axis fast path); TYPE 1: circular table (per-cell candidate lists).
 // Both fall back to the exhaustive search for inputs their fast path does not cover.
 template <int TYPE>
@@ -187,6 +195,10 @@ __global__ __launch_bounds__(kCBlock) void k_c256_demod(C256Streams st, uint32_t
   __shared__ float lxp[18], lyp[18];  // rectangular levels, padded with +inf (demod_rect_fast)
   __shared__ uint16_t cstart[TYPE == 0 ? 1 : kCellGrid * kCellGrid + 1];
   __shared__ uint8_t cidx[TYPE == 0 ? 4 : kMaxCellEntries];
+  // circular full tiles: the tile's decisions, and per wave the symbols whose search is not finished
+  // after the first four candidates (see below)
+  __shared__ uint16_t otile[TYPE == 0 ? 1 : kCBlock * kCSym / 2];
+  __shared__ uint16_t cq[TYPE == 0 ? 1 : kCBlock / 64][TYPE == 0 ? 1 : 64 * kCSym];
   const float2* tsrc = c_qpsk256_tables[TYPE];
   for (uint32_t i = threadIdx.x; i < 256; i += kCBlock) tab[i] = tsrc[i];
   if (TYPE == 0 && threadIdx.x < 18) {
@@ -247,12 +259,58 @@ __global__ __launch_bounds__(kCBlock) void k_c256_demod(C256Streams st, uint32_t
       return demod_exhaustive(tab, r);
     }
   };
+  // circular, first step: a cell whose candidate list holds a single point decides the symbol without
+  // any distance; false for longer lists and outside the grid
+  auto circ_first = [&](float2 r, uint32_t& idx) -> bool {
+    const float fx = (r.x + cR) * inv_cs, fy = (r.y + cR) * inv_cs;
+    if (!(cR > 0.0f && fx >= 0.0f && fy >= 0.0f && fx < (float)kCellGrid && fy < (float)kCellGrid)) return false;
+    const int c = (int)fy * kCellGrid + (int)fx;
+    const uint32_t b = cstart[c], e = cstart[c + 1];
+    idx = cidx[b];
+    return e - b == 1u;
+  };
   // grid-stride over 4096-symbol tiles, so the LDS tables are staged once per workgroup
   const uint32_t tiles = (uint32_t)((n + (uint64_t)kCBlock * kCSym - 1) / ((uint64_t)kCBlock * kCSym));
   const bool aligned = (reinterpret_cast<uintptr_t>(in) & 15u) == 0 && (reinterpret_cast<uintptr_t>(out) & 1u) == 0;
   for (uint32_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
     const uint64_t base = (uint64_t)tile * kCBlock * kCSym;
-    if (aligned && base + kCBlock * kCSym <= n) {
+    if (TYPE == 1 && aligned && base + kCBlock * kCSym <= n) {
+      // Circular full tile. The candidate lists average 1.6 entries but the longest list in a wave is
+      // 8-9, so walking each symbol's list in lockstep leaves most lanes idle. Here every symbol first
+      // looks up its cell (single-point cells are decided there); the wave's other symbols go to a
+      // wave queue in LDS, which its 64 lanes then drain one symbol each (whole list or exhaustive).
+      const float4* src = reinterpret_cast<const float4*>(in + base);
+      float4 v[kCSym / 2];
+#pragma unroll
+      for (int q = 0; q < kCSym / 2; ++q) v[q] = src[q * kCBlock + threadIdx.x];
+      const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+      uint16_t* qw = cq[TYPE == 0 ? 0 : w];
+      uint32_t qn = 0;  // wave-uniform
+#pragma unroll
+      for (int q = 0; q < kCSym / 2; ++q) {
+        const uint32_t pair = q * kCBlock + threadIdx.x;
+        uint32_t i0 = 0, i1 = 0;
+        const bool d0 = circ_first(make_float2(v[q].x, v[q].y), i0);
+        const bool d1 = circ_first(make_float2(v[q].z, v[q].w), i1);
+        otile[pair] = (uint16_t)(i0 | (i1 << 8));
+        const uint64_t m0 = __ballot(!d0), m1 = __ballot(!d1);
+        const uint64_t below = (1ull << lane) - 1ull;
+        if (!d0) qw[qn + __popcll(m0 & below)] = (uint16_t)(2u * pair);
+        qn += (uint32_t)__popcll(m0);
+        if (!d1) qw[qn + __popcll(m1 & below)] = (uint16_t)(2u * pair + 1u);
+        qn += (uint32_t)__popcll(m1);
+      }
+      wave_sync();  // the queue and the first-step decisions come from other lanes of the wave
+      uint8_t* ob = reinterpret_cast<uint8_t*>(otile);
+      for (uint32_t i = lane; i < qn; i += 64) {
+        const uint32_t pos = qw[i];
+        ob[pos] = (uint8_t)demod(in[base + pos]);
+      }
+      wave_sync();
+      uint16_t* dst = reinterpret_cast<uint16_t*>(out + base);
+#pragma unroll
+      for (int q = 0; q < kCSym / 2; ++q) dst[q * kCBlock + threadIdx.x] = otile[q * kCBlock + threadIdx.x];
+    } else if (aligned && base + kCBlock * kCSym <= n) {
       // full, aligned tile: lane t of slot q reads symbol pair q * kCBlock + t (coalesced 1 KB loads)
       const float4* src = reinterpret_cast<const float4*>(in + base);
       uint16_t* dst = reinterpret_cast<uint16_t*>(out + base);
@@ -275,8 +333,8 @@ __global__ __launch_bounds__(kCBlock) void k_c256_demod(C256Streams st, uint32_t
   }
 }
 
-// circular demodulation workgroups per stream (grid-stride): 4 resident per CU x 256 CUs
-constexpr uint32_t kCircBlocks = 1024;
+// circular demodulation workgroups per stream (grid-stride): 3 resident per CU x 256 CUs (52 KB LDS)
+constexpr uint32_t kCircBlocks = 768;
 
 static hipError_t c256_launch(bool modulate, const C256Streams& st, int nstreams, uint32_t n, uint32_t type,
                               int32_t device, hipStream_t stream) {
@@ -291,8 +349,8 @@ static hipError_t c256_launch(bool modulate, const C256Streams& st, int nstreams
   if (modulate) {
     k_c256_mod<<<grid, dim3(kCBlock), 0, stream>>>(st, n, type);
   } else {
-    // rectangular: one workgroup per tile; circular: one resident round of workgroups (its cell lists
-    // take < 40 KB of LDS, 4 workgroups per CU) striding over the tiles
+    // rectangular: one workgroup per tile; circular: one resident round of workgroups (cell lists,
+    // decision tile and wave queues take 52 KB of LDS, 3 workgroups per CU) striding over the tiles
     const dim3 dgrid(type == 0 ? blocks : std::min<uint32_t>(blocks, kCircBlocks), (uint32_t)nstreams);
     if (type == 0) {
       k_c256_demod<0><<<dgrid, dim3(kCBlock), 0, stream>>>(st, n);

@@ -784,3 +784,156 @@ def test_iir_large_array(cuda):
     y = _iir(cuda, b, a, x)
     want, _, _ = o.iir(b, a, x)
     assert np.max(np.abs(y - want)) < 1e-6 * np.max(np.abs(want))
+
+
+# ------------------------------------------------------------------------------------------------
+# ArithmeticTest (reference tests/test_arithmetic.cpp)
+# ------------------------------------------------------------------------------------------------
+def _rand(n, cplx, seed, scale=1.0):
+    rng = np.random.default_rng(seed)
+    v = (rng.uniform(-scale, scale, (n, 2) if cplx else n)).astype(np.float32)
+    return v.view(np.complex64).reshape(n) if cplx else v
+
+
+@pytest.mark.parametrize("case,cplx_in,c", [("FloatFloat", False, 1.25), ("ComplexComplex", True, 0.5 - 2j),
+                                            ("ComplexFloat", True, 1.25), ("FloatComplex", False, -0.75 + 0.5j)])
+def test_arith_add_const(cuda, case, cplx_in, c):
+    """test_arithmetic.cpp:59, 74, 90, 106 AddConst{FloatFloat, ComplexComplex, ComplexFloat,
+    FloatComplex}Test -- x + c with the reference operators: a real constant on complex input adds to
+    the real part only, a complex constant on real input gives (x + c.re, c.im) (add_const.cu)."""
+    from gsdr_amd import ops
+
+    x = _rand(5000, cplx_in, 1)
+    got = ops.add_const(dev(x, cuda), c).cpu().numpy()
+    if cplx_in and not isinstance(c, complex):
+        want = (x.real + np.float32(c)) + 1j * x.imag
+    elif isinstance(c, complex):
+        want = (x.real + np.float32(c.real)) + 1j * ((x.imag if cplx_in else 0) + np.float32(c.imag))
+    else:
+        want = x + np.float32(c)
+    assert np.array_equal(got, np.asarray(want, got.dtype))
+
+
+@pytest.mark.parametrize("case", ["ComplexComplex", "FloatFloat", "ComplexFloat"])
+def test_arith_multiply(cuda, case):
+    """test_arithmetic.cpp:122, 141, 156 Multiply{ComplexComplex, FloatFloat, ComplexFloat}Test --
+    element-wise products, bit-exact to the oracle's cuCmulf / c*r order."""
+    from gsdr_amd import ops
+
+    a = _rand(4099, case != "FloatFloat", 2)
+    b = _rand(4099, case == "ComplexComplex", 3)
+    got = ops.multiply(dev(a, cuda), dev(b, cuda)).cpu().numpy()
+    assert np.array_equal(got, o.multiply(a, b))
+
+
+def test_arith_magnitude_abs_add_to_magnitude(cuda):
+    """test_arithmetic.cpp:175 MagnitudeTest, :189 AbsTest, :208 AddToMagnitudeTest -- |x| (hypot),
+    fabs, and x scaled so its magnitude grows by c with the phase kept."""
+    from gsdr_amd import ops
+
+    x = _rand(3000, True, 4)
+    mag = ops.magnitude(dev(x, cuda)).cpu().numpy()
+    assert np.max(np.abs(mag - np.abs(x.astype(np.complex128)))) < 2e-7
+    r = _rand(3000, False, 5)
+    assert np.array_equal(ops.abs_(dev(r, cuda)).cpu().numpy(), np.abs(r))
+    grown = ops.add_to_magnitude(dev(x, cuda), 0.5).cpu().numpy()
+    assert np.max(np.abs(np.abs(grown) - (np.abs(x) + 0.5))) < 1e-6
+    assert np.max(np.abs(np.angle(grown) - np.angle(x))) < 1e-5
+
+
+def test_arith_zero_input_and_edge_cases(cuda):
+    """test_arithmetic.cpp:234 ZeroInputTest, :256 EdgeCasesTest -- zeros stay exact (0 + c, 0 * x,
+    |0| = 0), zero-length calls succeed and write nothing, exactly n elements are written."""
+    from gsdr_amd import ops
+
+    z = torch.zeros(1000, dtype=torch.complex64, device=cuda)
+    assert torch.equal(ops.add_const(z, 2.0).real, torch.full((1000,), 2.0, device=cuda))
+    assert torch.all(ops.multiply(z, dev(_rand(1000, True, 6), cuda)) == 0)
+    assert torch.all(ops.magnitude(z) == 0)
+    buf = torch.full((8,), 5.0, device=cuda)
+    ops.abs_(torch.full((3,), -1.0, device=cuda), out=buf[:3])
+    torch.cuda.synchronize()
+    assert buf.tolist() == [1.0, 1.0, 1.0, 5.0, 5.0, 5.0, 5.0, 5.0]
+    assert ops.abs_(torch.empty(0, device=cuda)).numel() == 0
+
+
+def test_arith_large_numbers_and_special_values(cuda):
+    """test_arithmetic.cpp:275 LargeNumbersTest, :289 SpecialValuesTest -- magnitudes near FLT_MAX do
+    not overflow in hypot; inf / nan propagate as IEEE arithmetic does (|-inf| = inf, |nan| = nan)."""
+    from gsdr_amd import ops
+
+    big = np.array([3e38 + 3e38j, -2e38 + 1e38j], np.complex64)
+    mag = ops.magnitude(dev(big, cuda)).cpu().numpy()
+    assert np.isinf(mag[0]) and abs(mag[1] / np.float32(2.2360680e38) - 1) < 1e-6
+    sp = np.array([np.inf, -np.inf, np.nan, -0.0, 1e-45], np.float32)
+    got = ops.abs_(dev(sp, cuda)).cpu().numpy()
+    assert got[0] == np.inf and got[1] == np.inf and np.isnan(got[2])
+    assert got[3] == 0.0 and not np.signbit(got[3]) and got[4] == np.float32(1e-45)
+
+
+# ------------------------------------------------------------------------------------------------
+# ConversionTest (reference tests/test_conversion.cpp): max(-1, v / 127) (conversion.cu:26)
+# ------------------------------------------------------------------------------------------------
+def test_conversion_int8_to_float(cuda):
+    """test_conversion.cpp:47 Int8ToFloatTest, :63 RangeTest, :108 PrecisionTest, :180 BoundaryTest --
+    every int8 value maps to the IEEE quotient v / 127 (so 127 -> 1, 0 -> 0) and -128 clamps to -1."""
+    from gsdr_amd import ops
+
+    v = np.arange(-128, 128, dtype=np.int8)
+    got = ops.int8_to_norm_float(dev(v, cuda)).cpu().numpy()
+    want = np.maximum(np.float32(-1), v.astype(np.float32) / np.float32(127))
+    assert np.array_equal(got, want)
+    assert got[0] == -1.0 and got[255] == 1.0 and got[128] == 0.0
+    assert np.all(got >= -1.0) and np.all(got <= 1.0)
+
+
+def test_conversion_zero_large_deterministic_statistical(cuda):
+    """test_conversion.cpp:79 ZeroLengthTest, :88 LargeArrayTest, :126 StatisticalTest, :161
+    DeterministicTest -- zero length is a no-op; 2^24 + 3 values convert exactly, twice identically,
+    and uniform int8 input gives the mean of its 256 levels (-1/256: -128 clamps to -1) and variance
+    ~1/3."""
+    from gsdr_amd import ops
+
+    assert ops.int8_to_norm_float(torch.empty(0, dtype=torch.int8, device=cuda)).numel() == 0
+    v = torch.randint(-128, 128, ((1 << 24) + 3,), dtype=torch.int8, device=cuda)
+    a, b = ops.int8_to_norm_float(v), ops.int8_to_norm_float(v)
+    assert torch.equal(a, b)
+    lut = np.maximum(np.float32(-1), np.arange(-128, 128, dtype=np.float32) / np.float32(127))
+    assert np.array_equal(a.cpu().numpy(), lut[v.cpu().numpy().astype(np.int64) + 128])
+    mean, var = float(a.mean()), float(a.var())
+    assert abs(mean - (-1 / 256)) < 1e-3 and abs(var - float(np.var(lut))) < 5e-3
+
+
+# ------------------------------------------------------------------------------------------------
+# TrigTest (reference tests/test_trig.cpp): out[k] = cos(phiBegin + k (phiEnd - phiBegin) / n),
+# complex: (cos, sin) (trig.cu:20-45, 55)
+# ------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("complex_out", [False, True])
+@pytest.mark.parametrize("phi0,phi1,n", [(0.0, 2 * np.pi, 1000), (-3.0, 1.0, 777), (-100.0, -40.0, 5000),
+                                         (0.0, 1000.0, 100000), (1.0, 1.0, 64)])
+def test_trig_cosine(cuda, complex_out, phi0, phi1, n):
+    """test_trig.cpp:48 CosineFloatTest, :62 CosineComplexTest, :77 PhaseRangeTest, :148 LargeRangeTest,
+    :185 NegativePhasesTest, :200 ComplexLargeTest -- the ramp against cos / sin of the same float
+    phase; values within 2e-6 and, for the complex form, on the unit circle (:216 UnitCircleTest)."""
+    from gsdr_amd import ops
+
+    got = ops.cosine(phi0, phi1, n, complex_out, device=cuda).cpu().numpy()
+    want = o.cosine(phi0, phi1, n, complex_out)
+    assert np.max(np.abs(got.astype(np.complex128) - want)) < 2e-6
+    if complex_out:
+        assert np.max(np.abs(np.abs(got.astype(np.complex128)) - 1)) < 1e-6
+
+
+def test_trig_known_values_edge_and_consistency(cuda):
+    """test_trig.cpp:115 KnownValuesTest, :101 EdgeCasesTest, :131 ConsistencyTest, :169 PrecisionTest --
+    a ramp from 0 to 2 pi over 4 samples gives cos at 0, pi/2, pi, 3 pi/2 (the reference expected values
+    of a different ramp, DESIGN.md section 8); one sample is cos(phiBegin); zero samples is a no-op;
+    repeated calls are identical."""
+    from gsdr_amd import ops
+
+    four = ops.cosine(0.0, 2 * np.pi, 4, False, device=cuda).cpu().numpy()
+    assert np.allclose(four, [1, 0, -1, 0], atol=1e-6)
+    assert abs(ops.cosine(0.5, 9.0, 1, False, device=cuda).cpu().numpy()[0] - np.cos(np.float32(0.5))) < 1e-7
+    assert ops.cosine(0.0, 1.0, 0, True, device=cuda).numel() == 0
+    a = ops.cosine(-2.0, 50.0, 10000, True, device=cuda)
+    assert torch.equal(a, ops.cosine(-2.0, 50.0, 10000, True, device=cuda))

@@ -175,6 +175,46 @@ def time_abi(torch, fn, argsets, reps=50, settle=400):
     return s.elapsed_time(e) / reps * 1e-3
 
 
+def fm_channel(torch, n, device, seed, n0=0):
+    """Config 3's input generated on the device: constant-envelope FM, carrier +0.1 fs,
+    message tone 0.001 fs, peak deviation 0.02 fs, amplitude 1, plus AWGN sigma 0.05 per axis; samples
+    n0 .. n0 + n - 1 of the channel (consecutive batches continue the same signal)."""
+    import math
+
+    idx = torch.arange(n0, n0 + n, dtype=torch.float64, device=device)
+    ph = 2 * math.pi * 0.1 * idx + (0.02 / 0.001) * torch.sin(2 * math.pi * 0.001 * idx)
+    del idx
+    x = torch.polar(torch.ones_like(ph), ph).to(torch.complex64)
+    del ph
+    g = torch.Generator(device=device).manual_seed(seed)
+    x += (torch.randn(2 * n, dtype=torch.float32, device=device, generator=g) * 0.05).view(torch.complex64)
+    return x
+
+
+def fm_multi_gpu(torch, device, taps, rank, world, steps):
+    """Config 4: one config-3 FM channel per GPU (seed 0x5EED + rank), no exchange; every rank times its
+    own launches between barriers and the slowest rank sets the aggregate."""
+    from gsdr_amd import abi
+
+    fs, tune, chan, dev_hz = 1.0e6, 0.0, 1.0e5, 2.0e4
+    n_fm = (1 << 24) - 1
+    n_in = n_fm * DECIM + TAPS
+    stream = torch.cuda.current_stream(device).cuda_stream
+    xs = [fm_channel(torch, n_in, device, channel_seed(rank) + 1000 * k, k * n_in) for k in range(ROTATE)]
+    y = torch.empty(n_fm, dtype=torch.float32, device=device)
+    argsets = [(fs, tune, chan, dev_hz, DECIM, 0, taps.data_ptr(), TAPS, x.data_ptr(), y.data_ptr(), n_fm,
+                device.index, stream) for x in xs]
+    torch.cuda.synchronize()
+    barrier()
+    t = time_abi(torch, abi.lib.gsdrFmDemod, argsets, reps=steps)
+    t_max = reduce_max(t, device)
+    del xs, y
+    return {"config": "BASELINE configs[3]: one NCO + 127-tap FIR + FM channel (67,108,987 samples of config 3's "
+                      "signal) per GPU, independent channels, no collective",
+            "n_gpus": world, "us_per_launch_max_over_ranks": round(t_max * 1e6, 2),
+            "aggregate_msamples_per_s": round(world * n_in / t_max / 1e6, 1)}
+
+
 def secondary_configs(torch, ops, device, taps):
     """Config 3 (fused NCO + FIR + FM, 64 M samples), the int8 I/Q front end on
     the config-2 and config-3 shapes, and config 5 (QPSK256 16 M symbols): kernel times from HIP
@@ -191,13 +231,15 @@ def secondary_configs(torch, ops, device, taps):
     n_in = n_fm * DECIM + TAPS
     g = torch.Generator(device=device).manual_seed(0x5EED)
     stream = torch.cuda.current_stream(device).cuda_stream
-    xs = [(torch.rand(2 * n_in, device=device, generator=g) * 2 - 1).view(torch.complex64) for _ in range(ROTATE)]
+    # config 3's signal (constant-envelope FM + AWGN), consecutive batches of one channel
+    xs = [fm_channel(torch, n_in, device, 0x5EED + 1000 * k, k * n_in) for k in range(ROTATE)]
     y = torch.empty(n_fm, dtype=torch.float32, device=device)
     argsets = [(fs, tune, chan, dev_hz, DECIM, 0, taps.data_ptr(), TAPS, x.data_ptr(), y.data_ptr(), n_fm,
                 device.index, stream) for x in xs]
     t = time_abi(torch, abi.lib.gsdrFmDemod, argsets)
     b = 8 * n_in + 4 * n_fm + 4 * TAPS
-    out["fm_chain"] = {"config": "NCO + 127-tap FIR (D=4) + FM discriminator, 67,108,987 samples (BASELINE configs[2])",
+    out["fm_chain"] = {"config": "NCO + 127-tap FIR (D=4) + FM discriminator, 67,108,987 samples of constant-envelope "
+                                 "FM + AWGN (BASELINE configs[2])",
                        "us_per_launch": round(t * 1e6, 2), "msamples_per_s": round(n_in / t / 1e6, 1),
                        "alg_gbps": round(b / t / 1e9, 1), "alg_bytes_per_launch": b}
     # multi-channel chain: C channels from one read of the input
@@ -374,6 +416,9 @@ def main():
     wall_max = reduce_max(wall, device)
     kern_s = ev0.elapsed_time(ev1) / args.steps * 1e-3  # mean launch duration (back-to-back launches)
     kern_s_max = reduce_max(kern_s, device)
+    fm_multi = None
+    if world > 1 and not args.no_secondary:
+        fm_multi = fm_multi_gpu(torch, device, taps, rank, world, args.steps)
 
     if rank != 0:
         if world > 1:
@@ -429,6 +474,8 @@ def main():
         pass
     if world == 1 and not args.no_secondary:
         line["secondary"] = secondary_configs(torch, ops, device, taps)
+    if fm_multi is not None:
+        line["secondary"] = {"fm_chain_multi_gpu": fm_multi}
     if world == 1 and not args.no_cpu_baseline:
         threads = min(16, os.cpu_count() or 1)
         line["cpu_baseline"] = cpu_baseline(x.cpu().numpy(), taps_np, threads)

@@ -55,6 +55,8 @@ def reduce_max(value: float, device) -> float:
 
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return value
+    if dist.get_backend() == "gloo":
+        device = "cpu"
     t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
@@ -354,10 +356,17 @@ def main():
         if world == 1 and args.gpus > 1:
             sys.exit("--gpus N > 1 must be launched with torch.distributed.run (one process per GPU)")
         raise SystemExit(f"WORLD_SIZE={world} does not match --gpus {args.gpus}")
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
+    # BENCH_REHEARSE=1 (rehearsal only, never a reported number): gloo instead of RCCL and rank r on
+    # cuda:(r mod device_count), so the N > 1 code path can run on a one-GPU box with ranks sharing it.
+    rehearse = os.environ.get("BENCH_REHEARSE") == "1"
+    dev_index = local_rank % torch.cuda.device_count() if rehearse else local_rank
+    torch.cuda.set_device(dev_index)
+    device = torch.device("cuda", dev_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=device)
 
     from gsdr_amd import ops
     from gsdr_amd.signals import lowpass_taps
@@ -381,11 +390,11 @@ def main():
     stream = torch.cuda.current_stream(device).cuda_stream
     if args.variant >= 0:
         fn = abi.lib.gsdrxFirFCVariant
-        argsets = [(args.variant, DECIM, taps.data_ptr(), TAPS, xb.data_ptr(), y.data_ptr(), N_OUT, local_rank,
+        argsets = [(args.variant, DECIM, taps.data_ptr(), TAPS, xb.data_ptr(), y.data_ptr(), N_OUT, dev_index,
                     stream) for xb in xs]
     else:
         fn = abi.lib.gsdrFirFC
-        argsets = [(DECIM, taps.data_ptr(), TAPS, xb.data_ptr(), y.data_ptr(), N_OUT, local_rank, stream)
+        argsets = [(DECIM, taps.data_ptr(), TAPS, xb.data_ptr(), y.data_ptr(), N_OUT, dev_index, stream)
                    for xb in xs]
 
     def step():
@@ -464,6 +473,8 @@ def main():
             "alg_tflops": round(ALG_FLOP / kern_s / 1e12, 2),
         },
     }
+    if rehearse:
+        line["rehearsal"] = "BENCH_REHEARSE=1: gloo, ranks sharing GPUs; not a measurement"
     if pmc:
         line["roofline"]["traffic_source"] = os.path.relpath(PMC_SUMMARY, ROOT)
     try:

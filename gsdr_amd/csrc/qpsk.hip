@@ -56,7 +56,7 @@ __global__ __launch_bounds__(kQBlock) void k_qpsk_mod(QpskStreams st, uint32_t n
   const uint64_t s0 = base + (uint64_t)threadIdx.x * kQSym;
   if (s0 >= n) return;
   const uint64_t b0 = s0 >> 2;
-  const uint32_t nbytes = (uint32_t)((n + 3u) >> 2);
+  const uint32_t nbytes = (uint32_t)(((uint64_t)n + 3u) >> 2);
   uint32_t word = 0;
   if ((reinterpret_cast<uintptr_t>(in + b0) & 3u) == 0 && b0 + 4 <= nbytes) {
     word = *reinterpret_cast<const uint32_t*>(in + b0);
@@ -153,7 +153,8 @@ static hipError_t qpsk_launch(bool modulate, const QpskStreams& st, int nstreams
   }
   DeviceScope scope(device);
   if (scope.status() != hipSuccess) return scope.status();
-  const uint32_t blocks = ceil_div<uint32_t>(ceil_div<uint32_t>(n, kQSym), kQBlock);
+  // in 64 bits: n + kQSym - 1 wraps a uint32_t for n near 2^32 (numSymbols is uint32_t)
+  const uint32_t blocks = (uint32_t)ceil_div<uint64_t>(ceil_div<uint64_t>(n, kQSym), kQBlock);
   const dim3 grid(blocks, (uint32_t)nstreams);
   if (modulate) {
     k_qpsk_mod<<<grid, dim3(kQBlock), 0, stream>>>(st, n, a);

@@ -344,7 +344,8 @@ static hipError_t c256_launch(bool modulate, const C256Streams& st, int nstreams
   }
   DeviceScope scope(device);
   if (scope.status() != hipSuccess) return scope.status();
-  const uint32_t blocks = ceil_div<uint32_t>(ceil_div<uint32_t>(n, kCSym), kCBlock);
+  // in 64 bits: n + kCSym - 1 wraps a uint32_t for n near 2^32 (numSymbols is uint32_t)
+  const uint32_t blocks = (uint32_t)ceil_div<uint64_t>(ceil_div<uint64_t>(n, kCSym), kCBlock);
   const dim3 grid(blocks, (uint32_t)nstreams);
   if (modulate) {
     k_c256_mod<<<grid, dim3(kCBlock), 0, stream>>>(st, n, type);

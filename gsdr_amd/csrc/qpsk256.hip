@@ -41,7 +41,7 @@ __constant__ float2 c_qpsk256_tables[2][256];
 constexpr int kCellGrid = 96;
 constexpr int kMaxCellEntries = 19456;  // 18,764 used by the circular table (any amplitude); LDS < 40 KB
 constexpr double kCellSpan = 1.3;  // grid half-width R = 1.3 * max |c|: noisy symbols stay on the grid
-struct CircCells {
+struct alignas(16) CircCells {
   float R;
   float inv_cs;  // kCellGrid / (2 R)
   uint16_t start[kCellGrid * kCellGrid + 1];
@@ -193,8 +193,10 @@ template <int TYPE>
 __global__ __launch_bounds__(kCBlock) void k_c256_demod(C256Streams st, uint32_t n) {
   __shared__ float2 tab[256];
   __shared__ float lxp[18], lyp[18];  // rectangular levels, padded with +inf (demod_rect_fast)
-  __shared__ uint16_t cstart[TYPE == 0 ? 1 : kCellGrid * kCellGrid + 1];
-  __shared__ uint8_t cidx[TYPE == 0 ? 4 : kMaxCellEntries];
+  // the circular cell lists: an LDS image of g_circ_cells (start offsets and candidate indices)
+  __shared__ uint4 ccells[TYPE == 0 ? 1 : sizeof(CircCells) / 16];
+  const uint16_t* cstart = reinterpret_cast<const CircCells*>(ccells)->start;
+  const uint8_t* cidx = reinterpret_cast<const CircCells*>(ccells)->idx;
   // circular full tiles: the tile's decisions, and per wave the symbols whose search is not finished
   // after the first four candidates (see below)
   __shared__ uint16_t otile[TYPE == 0 ? 1 : kCBlock * kCSym / 2];
@@ -207,10 +209,18 @@ __global__ __launch_bounds__(kCBlock) void k_c256_demod(C256Streams st, uint32_t
     lyp[threadIdx.x] = (k < 0 || k > 15) ? INFINITY : tsrc[k].y;
   }
   if (TYPE != 0 && g_circ_cells.R > 0.0f) {  // the circular candidate lists, into LDS
-    for (uint32_t i = threadIdx.x; i <= (uint32_t)(kCellGrid * kCellGrid); i += kCBlock) cstart[i] = g_circ_cells.start[i];
-    const uint32_t total = g_circ_cells.start[kCellGrid * kCellGrid];
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(g_circ_cells.idx);
-    for (uint32_t i = threadIdx.x; i < (total + 3) / 4; i += kCBlock) reinterpret_cast<uint32_t*>(cidx)[i] = src[i];
+    // 16-byte copies, all issued before the first LDS store (~37 KB: ten loads a lane; the per-entry
+    // 2-byte copy loop it replaces waited on each load in turn and cost ~5 % of the kernel)
+    constexpr uint32_t kWords = sizeof(CircCells) / 16, kFull = kWords / kCBlock;
+    const uint4* src = reinterpret_cast<const uint4*>(&g_circ_cells);
+    uint4 w[kFull], wt = make_uint4(0u, 0u, 0u, 0u);
+    const uint32_t it = kFull * kCBlock + threadIdx.x;
+#pragma unroll
+    for (uint32_t k = 0; k < kFull; ++k) w[k] = src[k * kCBlock + threadIdx.x];
+    if (it < kWords) wt = src[it];
+#pragma unroll
+    for (uint32_t k = 0; k < kFull; ++k) ccells[k * kCBlock + threadIdx.x] = w[k];
+    if (it < kWords) ccells[it] = wt;
   }
   __syncthreads();
   const float2* __restrict__ in = reinterpret_cast<const float2*>(st.in[blockIdx.y]);

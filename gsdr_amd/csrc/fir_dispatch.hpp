@@ -1,8 +1,9 @@
 // gsdr-mi355x: host-side choice of FIR kernel instantiation for a job (FIR, FM chain or AM chain).
 //
 // Fast paths (tiled, LDS-staged, register-windowed; see fir_engine.hpp):
-//   complex input: D in {2, 4, 8} polyphase kernel, D == 1 contiguous-window kernel
-//   real input:    D in {4, 8}    polyphase kernel, D in {1, 2} contiguous-window kernel
+//   complex input: D in {2, 4, 6, 8, 10, 12, 16} polyphase kernel, D in {1, 3, 5, 7} contiguous-window
+//   real input:    D in {4, 8, 12, 16} polyphase kernel, D in {1, 2, 3, 5, 6, 7, 10} contiguous-window
+//   int8 I/Q:      D in {2, 4, 8} polyphase kernel
 // Everything else (other decimations, tap spans that would not fit the LDS budget) runs the generic
 // one-output-per-thread kernel, which is correct for any shape.
 #pragma once
@@ -267,6 +268,57 @@ hipError_t launch_poly_default(const FirJob& j, hipStream_t s) {
   return launch_poly<TapT, InT, D, R, JC, WG, MODE, 0, true>(j, s);
 }
 
+template <class InT, int D, int R, int IC, int WG>
+constexpr bool contig_fits_lds_at_t127() {
+  constexpr uint32_t span = (127 + IC - 1) / IC * IC;
+  return poly_lds_bytes<InT, D, R, WG>(span, kModeFm) <= kMaxTileLds;
+}
+
+template <class TapT, class InT, int D, int R, int IC, int WG, int MODE>
+hipError_t launch_contig_default(const FirJob& j, hipStream_t s) {
+  static_assert(contig_fits_lds_at_t127<InT, D, R, IC, WG>(), "default contiguous shape exceeds the LDS budget");
+  return launch_contig<TapT, InT, D, R, IC, WG, MODE>(j, s);
+}
+
+// Decimations without a polyphase column layout (odd D, or real D not a multiple of 4) and the large
+// even ones: the contiguous-window kernel with R outputs a thread (R * D whole granules) or a one-row
+// polyphase tile. The one-output-per-thread generic kernel ran these 10-20x slower.
+template <class TapT, class InT, int MODE>
+hipError_t launch_other_d(const FirJob& j, hipStream_t s) {
+  constexpr bool kComplexIn = SampleT<InT>::kPerGranule == 2;
+  switch (j.D) {
+    // (tap chunks of 24-40: every chunk costs one scalar tap-load wait)
+    case 3:
+      return launch_contig_default<TapT, InT, 3, 4, (kComplexIn ? 24 : 36), 256, MODE>(j, s);
+    case 5:
+      return launch_contig_default<TapT, InT, 5, 4, (kComplexIn ? 20 : 40), 128, MODE>(j, s);
+    case 6:
+      if constexpr (kComplexIn) {
+        return launch_poly_default<TapT, InT, 6, 2, 8, 256, MODE>(j, s);
+      } else {
+        return launch_contig_default<TapT, InT, 6, 2, 36, 256, MODE>(j, s);
+      }
+    case 7:
+      return launch_contig_default<TapT, InT, 7, 4, 28, 128, MODE>(j, s);
+    case 10:
+      if constexpr (kComplexIn) {
+        return launch_poly_default<TapT, InT, 10, 2, 8, 256, MODE>(j, s);
+      } else {
+        return launch_contig_default<TapT, InT, 10, 2, 40, 256, MODE>(j, s);
+      }
+    case 12:
+      if constexpr (kComplexIn) {
+        return launch_poly_default<TapT, InT, 12, 2, 8, 256, MODE>(j, s);
+      } else {
+        return launch_poly_default<TapT, InT, 12, 4, 8, 128, MODE>(j, s);
+      }
+    case 16:
+      return launch_poly_default<TapT, InT, 16, (kComplexIn ? 2 : 4), 8, 128, MODE>(j, s);
+    default:
+      return launch_generic<TapT, InT, MODE>(j, s);
+  }
+}
+
 template <class TapT, class InT, int MODE>
 hipError_t launch_fir(const FirJob& j, hipStream_t s) {
   constexpr bool kComplexIn = SampleT<InT>::kPerGranule == 2;
@@ -302,12 +354,17 @@ hipError_t launch_fir(const FirJob& j, hipStream_t s) {
       case 8:
         return launch_poly_default<TapT, InT, 8, 2, 8, 256, MODE>(j, s);
       default:
-        return launch_generic<TapT, InT, MODE>(j, s);
+        return launch_other_d<TapT, InT, MODE>(j, s);
     }
   } else {
     switch (j.D) {
       case 1:
-        return launch_contig<TapT, InT, 1, 16, 32, 256, MODE>(j, s);
+        // complex taps on real samples: R = 16 with 32 two-float taps in flight spilled to scratch
+        if constexpr (!std::is_same<TapT, float>::value) {
+          return launch_contig<TapT, InT, 1, 8, 16, 256, MODE>(j, s);
+        } else {
+          return launch_contig<TapT, InT, 1, 16, 32, 256, MODE>(j, s);
+        }
       case 2:
         return launch_contig<TapT, InT, 2, 8, 16, 256, MODE>(j, s);
       case 4:
@@ -315,7 +372,7 @@ hipError_t launch_fir(const FirJob& j, hipStream_t s) {
       case 8:
         return launch_poly_default<TapT, InT, 8, 8, 8, 128, MODE>(j, s);
       default:
-        return launch_generic<TapT, InT, MODE>(j, s);
+        return launch_other_d<TapT, InT, MODE>(j, s);
     }
   }
 }

@@ -447,32 +447,34 @@ __device__ __forceinline__ void store16_nt(float4* p, float4 v) {
 template <class OutT, int R, bool NTS = false>
 __device__ __forceinline__ void store_fir(OutT* __restrict__ out, uint64_t k0, uint64_t N, const OutT (&acc)[R]) {
   constexpr int PER16 = 16 / sizeof(OutT);
-  static_assert(R % PER16 == 0, "R must fill whole 16-byte stores");
-  if (k0 + R <= N && (reinterpret_cast<uintptr_t>(out + k0) & 15u) == 0) {
-    float4* o = reinterpret_cast<float4*>(out + k0);
+  // 16-byte stores when R fills them (a thread's outputs are contiguous), else one output at a time
+  if constexpr (R % PER16 == 0) {
+    if (k0 + R <= N && (reinterpret_cast<uintptr_t>(out + k0) & 15u) == 0) {
+      float4* o = reinterpret_cast<float4*>(out + k0);
 #pragma unroll
-    for (int q = 0; q < R / PER16; ++q) {
-      float4 w;
-      if constexpr (PER16 == 2) {
-        w = make_float4(reinterpret_cast<const float2&>(acc[2 * q]).x, reinterpret_cast<const float2&>(acc[2 * q]).y,
-                        reinterpret_cast<const float2&>(acc[2 * q + 1]).x,
-                        reinterpret_cast<const float2&>(acc[2 * q + 1]).y);
-      } else {
-        w = make_float4(reinterpret_cast<const float&>(acc[4 * q]), reinterpret_cast<const float&>(acc[4 * q + 1]),
-                        reinterpret_cast<const float&>(acc[4 * q + 2]),
-                        reinterpret_cast<const float&>(acc[4 * q + 3]));
+      for (int q = 0; q < R / PER16; ++q) {
+        float4 w;
+        if constexpr (PER16 == 2) {
+          w = make_float4(reinterpret_cast<const float2&>(acc[2 * q]).x, reinterpret_cast<const float2&>(acc[2 * q]).y,
+                          reinterpret_cast<const float2&>(acc[2 * q + 1]).x,
+                          reinterpret_cast<const float2&>(acc[2 * q + 1]).y);
+        } else {
+          w = make_float4(reinterpret_cast<const float&>(acc[4 * q]), reinterpret_cast<const float&>(acc[4 * q + 1]),
+                          reinterpret_cast<const float&>(acc[4 * q + 2]),
+                          reinterpret_cast<const float&>(acc[4 * q + 3]));
+        }
+        if constexpr (NTS) {
+          store16_nt(o + q, w);
+        } else {
+          o[q] = w;
+        }
       }
-      if constexpr (NTS) {
-        store16_nt(o + q, w);
-      } else {
-        o[q] = w;
-      }
+      return;
     }
-  } else {
+  }
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      if (k0 + r < N) out[k0 + r] = acc[r];
-    }
+  for (int r = 0; r < R; ++r) {
+    if (k0 + r < N) out[k0 + r] = acc[r];
   }
 }
 

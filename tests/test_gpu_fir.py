@@ -45,7 +45,7 @@ def run_fir(cuda, taps, x, D, N, x_offset=0):
 
 
 @pytest.mark.parametrize("T", [1, 8, 63, 127, 200])
-@pytest.mark.parametrize("D", [1, 2, 3, 4, 5, 8])
+@pytest.mark.parametrize("D", [1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 16])
 @pytest.mark.parametrize("tt", list(TYPES))
 def test_fir_parity(cuda, tt, D, T):
     N = 2 * 4096 + 37  # several tiles plus a ragged tail
@@ -66,7 +66,8 @@ def test_fir_ragged_sizes(cuda, tt, N):
     assert normwise_err(y, o.fir(taps, x, D, N), bound(taps, x, D, N)) <= FLOAT_TOL
 
 
-@pytest.mark.parametrize("tt,D", [("FC", 4), ("FC", 1), ("FF", 1), ("CC", 2), ("CF", 4), ("FF", 8)])
+@pytest.mark.parametrize("tt,D", [("FC", 4), ("FC", 1), ("FF", 1), ("CC", 2), ("CF", 4), ("FF", 8), ("FC", 3),
+                                  ("FF", 5), ("CC", 6), ("CF", 7), ("FC", 10), ("FF", 12), ("CF", 16)])
 def test_fir_unaligned_input(cuda, tt, D):
     """Caller passes input + 1 sample (streaming overlap): 8-/4-byte aligned only."""
     N, T = 3000, 63

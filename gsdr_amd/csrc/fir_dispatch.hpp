@@ -3,7 +3,7 @@
 // Fast paths (tiled, LDS-staged, register-windowed; see fir_engine.hpp):
 //   complex input: D in {2, 4, 6, 8, 10, 12, 16} polyphase kernel, D in {1, 3, 5, 7} contiguous-window
 //   real input:    D in {4, 8, 12, 16} polyphase kernel, D in {1, 2, 3, 5, 6, 7, 10} contiguous-window
-//   int8 I/Q:      D in {2, 4, 8} polyphase kernel
+//   int8 I/Q:      as complex input
 // Everything else (other decimations, tap spans that would not fit the LDS budget) runs the generic
 // one-output-per-thread kernel, which is correct for any shape.
 #pragma once
@@ -325,11 +325,14 @@ hipError_t launch_fir(const FirJob& j, hipStream_t s) {
   // the tiled kernels address taps through a 32-bit buffer descriptor
   if (j.T > (1u << 26)) return launch_generic<TapT, InT, MODE>(j, s);
   if constexpr (std::is_same<InT, Iq8>::value) {
-    // int8 I/Q: the polyphase kernel (even D keeps every staged dword 4-byte aligned), else generic
+    // int8 I/Q
     if constexpr (MODE == kModeFir) {
       if (j.D == 4 && j.variant >= 0) return launch_d4_int8(j, s);
     }
+    // the float-input shapes, so int8 and float inputs of one decimation give bit-identical outputs
     switch (j.D) {
+      case 1:
+        return launch_contig<TapT, InT, 1, 8, 16, 256, MODE>(j, s);
       case 2:
         return launch_poly_default<TapT, InT, 2, 8, 16, 128, MODE>(j, s);
       case 4:
@@ -337,7 +340,7 @@ hipError_t launch_fir(const FirJob& j, hipStream_t s) {
       case 8:
         return launch_poly_default<TapT, InT, 8, 2, 8, 256, MODE>(j, s);
       default:
-        return launch_generic<TapT, InT, MODE>(j, s);
+        return launch_other_d<TapT, InT, MODE>(j, s);
     }
   } else if constexpr (kComplexIn) {
     switch (j.D) {

@@ -4,8 +4,9 @@
 //   complex input: D in {2, 4, 6, 8, 10, 12, 16} polyphase kernel, D in {1, 3, 5, 7} contiguous-window
 //   real input:    D in {4, 8, 12, 16} polyphase kernel, D in {1, 2, 3, 5, 6, 7, 10} contiguous-window
 //   int8 I/Q:      as complex input
-// Everything else (other decimations, tap spans that would not fit the LDS budget) runs the generic
-// one-output-per-thread kernel, which is correct for any shape.
+// Other decimations with T > D: runtime-decimation LDS tile kernel (k_fir_rt) while its tile fits the
+// LDS budget (complex D <= 31, real D <= 63 at T = 127). Everything else (D >= T, tap spans that would
+// not fit) runs the generic one-output-per-thread kernel, which is correct for any shape.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -268,6 +269,31 @@ hipError_t launch_poly_default(const FirJob& j, hipStream_t s) {
   return launch_poly<TapT, InT, D, R, JC, WG, MODE, 0, true>(j, s);
 }
 
+// Runtime-decimation tile kernel (k_fir_rt) for decimations without a compile-time shape, when the
+// tile fits the LDS budget and taps overlap between outputs (T > D); otherwise the generic kernel.
+template <class TapT, class InT, int MODE>
+hipError_t launch_rt(const FirJob& j, hipStream_t s) {
+  constexpr int IC = 16, WG = 256;
+  if (j.T <= j.D || j.D > 4096) return launch_generic<TapT, InT, MODE>(j, s);
+  const uint64_t nch = ceil_div<uint64_t>(j.T, (uint64_t)IC);
+  const size_t lds = rt_lds_bytes<InT>((uint32_t)j.D, (uint32_t)(nch * IC), WG, MODE);
+  if (lds > kMaxTileLds) return launch_generic<TapT, InT, MODE>(j, s);
+  FirParams p = make_params(j);
+  p.nch = (uint32_t)nch;
+  const uint32_t stride = (MODE == kModeFm) ? WG - 1 : WG;
+  p.tile_stride = stride;
+  const uint64_t tiles = ceil_div<uint64_t>(j.N, stride);
+  if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
+  constexpr uint64_t A = SampleT<InT>::kSrcAlign;
+  const bool vec = (reinterpret_cast<uintptr_t>(j.in) % A) == 0 && ((uint64_t)stride * j.D * sizeof(InT)) % A == 0;
+  if (vec) {
+    k_fir_rt<TapT, InT, IC, WG, true, MODE><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
+  } else {
+    k_fir_rt<TapT, InT, IC, WG, false, MODE><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
+  }
+  return launch_status();
+}
+
 template <class InT, int D, int R, int IC, int WG>
 constexpr bool contig_fits_lds_at_t127() {
   constexpr uint32_t span = (127 + IC - 1) / IC * IC;
@@ -315,7 +341,7 @@ hipError_t launch_other_d(const FirJob& j, hipStream_t s) {
     case 16:
       return launch_poly_default<TapT, InT, 16, (kComplexIn ? 2 : 4), 8, 128, MODE>(j, s);
     default:
-      return launch_generic<TapT, InT, MODE>(j, s);
+      return launch_rt<TapT, InT, MODE>(j, s);
   }
 }
 

@@ -816,6 +816,69 @@ __global__ __launch_bounds__(WG) void k_fir_contig(FirParams p) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// Kernel 2r: runtime-decimation tile kernel, for decimations without a compile-time shape. The tile's
+// input span is staged into LDS unpadded (NCO applied once per sample, as in the other tiled kernels)
+// and thread t computes output t of the tile from LDS, one sample read per tap (ds_read with the tap
+// as an immediate offset), in ascending tap order like the generic kernel. No register window (D is
+// not known at compile time), so it is bound by LDS reads (~T * sample bytes per output), which
+// still beats re-reading every sample T / D times through L1/L2.
+// ------------------------------------------------------------------------------------------------
+template <class TapT, class InT, int IC, int WG, bool VEC, int MODE>
+__global__ __launch_bounds__(WG) void k_fir_rt(FirParams p) {
+  using OutT = typename Product<TapT, InT>::type;
+  using LdsT = typename LdsSample<InT>::type;
+  constexpr int G = SampleT<InT>::kPerGranule;
+  constexpr int SB = 4;  // granules in flight per lane while staging
+
+  extern __shared__ __attribute__((aligned(16))) float4 lds[];
+  const InT* __restrict__ in = reinterpret_cast<const InT*>(p.in);
+  const uint32_t D = p.D;
+  const uint64_t out0 = (uint64_t)blockIdx.x * p.tile_stride;
+  const uint64_t S0 = out0 * D;
+  const uint32_t span = p.nch * IC;
+  const uint32_t NG = ((WG - 1) * D + span + G - 1) / G;
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t g0 = 0; g0 < NG; g0 += SB * WG) {
+    float4 v[SB];
+#pragma unroll
+    for (int k = 0; k < SB; ++k) {
+      const uint32_t g = g0 + k * WG + tid;
+      v[k] = g < NG ? load_granule<InT, VEC>(in, S0 + (uint64_t)g * G, p.L) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int k = 0; k < SB; ++k) {
+      const uint32_t g = g0 + k * WG + tid;
+      if (g < NG) lds[g] = stage_transform<InT, MODE>(v[k], (uint32_t)(S0 + (uint64_t)g * G), p);
+    }
+  }
+  __syncthreads();
+
+  OutT acc;
+  set_zero(acc);
+  const LdsT* __restrict__ xs = reinterpret_cast<const LdsT*>(lds) + tid * D;
+  for (uint32_t c = 0; c < p.nch; ++c) {
+    const TapBuf tb = tap_window<TapT>(p.taps, p.T, c * IC);
+    TapT tv[IC];
+#pragma unroll
+    for (int i = 0; i < IC; ++i) tv[i] = tap_at<TapT>(tb, i);
+    const LdsT* __restrict__ xc = xs + c * IC;
+#pragma unroll
+    for (int i = 0; i < IC; ++i) mac(acc, xc[i], tv[i]);
+  }
+  OutT accs[1] = {acc};
+  float2* ex = reinterpret_cast<float2*>(lds + NG);
+  tile_epilogue<MODE, OutT, 1, WG>(p, out0, accs, ex);
+}
+
+template <class InT>
+constexpr size_t rt_lds_bytes(uint32_t D, uint32_t span_samples, int wg, int mode) {
+  const uint32_t G = SampleT<InT>::kPerGranule;
+  size_t bytes = (size_t)(((uint32_t)(wg - 1) * D + span_samples + G - 1) / G) * 16u;
+  if (mode != kModeFir) bytes += ((size_t)wg * sizeof(float2) + 15) / 16 * 16;
+  return bytes;
+}
+
+// ------------------------------------------------------------------------------------------------
 // Kernel 3: generic fallback (any D, any T, any alignment): one output per thread straight from
 // global memory (L1/L2 absorb the overlap). Used only where the tiled kernels do not apply.
 // In FM mode each thread also computes the next FIR output.

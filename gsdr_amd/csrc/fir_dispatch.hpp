@@ -1,11 +1,13 @@
 // gsdr-mi355x: host-side choice of FIR kernel instantiation for a job (FIR, FM chain or AM chain).
 //
 // Fast paths (tiled, LDS-staged, register-windowed; see fir_engine.hpp):
-//   complex input: D in {2, 4, 6, 8, 10, 12, 16} polyphase kernel, D in {1, 3, 5, 7} contiguous-window
-//   real input:    D in {4, 8, 12, 16} polyphase kernel, D in {1, 2, 3, 5, 6, 7, 10} contiguous-window
+//   complex input: D in {2, 4, 6, 8, 10, 12, 16, 20, 24, 32, 40, 48, 64} polyphase kernel,
+//                  D in {1, 3, 5, 7} contiguous-window kernel
+//   real input:    D in {4, 8, 12, 16, 20, 24, 32, 40, 48, 64} polyphase kernel,
+//                  D in {1, 2, 3, 5, 6, 7, 10} contiguous-window kernel
 //   int8 I/Q:      as complex input
-// Other decimations with T > D: runtime-decimation LDS tile kernel (k_fir_rt) while its tile fits the
-// LDS budget (complex D <= 31, real D <= 63 at T = 127). Everything else (D >= T, tap spans that would
+// Other decimations with T > D: runtime-decimation LDS tile kernel (k_fir_rt) with 256, 128 or 64
+// outputs a tile, while the tile fits the LDS budget. Everything else (D >= T, tap spans that would
 // not fit) runs the generic one-output-per-thread kernel, which is correct for any shape.
 #pragma once
 
@@ -269,17 +271,14 @@ hipError_t launch_poly_default(const FirJob& j, hipStream_t s) {
   return launch_poly<TapT, InT, D, R, JC, WG, MODE, 0, true>(j, s);
 }
 
-// Runtime-decimation tile kernel (k_fir_rt) for decimations without a compile-time shape, when the
-// tile fits the LDS budget and taps overlap between outputs (T > D); otherwise the generic kernel.
-template <class TapT, class InT, int MODE>
-hipError_t launch_rt(const FirJob& j, hipStream_t s) {
-  constexpr int IC = 16, WG = 256;
-  if (j.T <= j.D || j.D > 4096) return launch_generic<TapT, InT, MODE>(j, s);
-  const uint64_t nch = ceil_div<uint64_t>(j.T, (uint64_t)IC);
-  const size_t lds = rt_lds_bytes<InT>((uint32_t)j.D, (uint32_t)(nch * IC), WG, MODE);
-  if (lds > kMaxTileLds) return launch_generic<TapT, InT, MODE>(j, s);
+// Runtime-decimation tile kernel (k_fir_rt) for decimations without a compile-time shape, when taps
+// overlap between outputs (T > D): the widest workgroup (256, 128 or 64 outputs a tile) whose tile fits
+// the LDS budget; otherwise the generic kernel.
+template <class TapT, class InT, int MODE, int WG>
+hipError_t launch_rt_wg(const FirJob& j, uint32_t nch, size_t lds, hipStream_t s) {
+  constexpr int IC = 16;
   FirParams p = make_params(j);
-  p.nch = (uint32_t)nch;
+  p.nch = nch;
   const uint32_t stride = (MODE == kModeFm) ? WG - 1 : WG;
   p.tile_stride = stride;
   const uint64_t tiles = ceil_div<uint64_t>(j.N, stride);
@@ -292,6 +291,21 @@ hipError_t launch_rt(const FirJob& j, hipStream_t s) {
     k_fir_rt<TapT, InT, IC, WG, false, MODE><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
   }
   return launch_status();
+}
+
+template <class TapT, class InT, int MODE>
+hipError_t launch_rt(const FirJob& j, hipStream_t s) {
+  constexpr int IC = 16;
+  if (j.T <= j.D || j.D > 4096) return launch_generic<TapT, InT, MODE>(j, s);
+  const uint32_t nch = (uint32_t)ceil_div<uint64_t>(j.T, (uint64_t)IC);
+  const uint32_t D = (uint32_t)j.D, span = nch * IC;
+  size_t lds = rt_lds_bytes<InT>(D, span, 256, MODE);
+  if (lds <= kMaxTileLds) return launch_rt_wg<TapT, InT, MODE, 256>(j, nch, lds, s);
+  lds = rt_lds_bytes<InT>(D, span, 128, MODE);
+  if (lds <= kMaxTileLds) return launch_rt_wg<TapT, InT, MODE, 128>(j, nch, lds, s);
+  lds = rt_lds_bytes<InT>(D, span, 64, MODE);
+  if (lds <= kMaxTileLds) return launch_rt_wg<TapT, InT, MODE, 64>(j, nch, lds, s);
+  return launch_generic<TapT, InT, MODE>(j, s);
 }
 
 template <class InT, int D, int R, int IC, int WG>
@@ -340,6 +354,20 @@ hipError_t launch_other_d(const FirJob& j, hipStream_t s) {
       }
     case 16:
       return launch_poly_default<TapT, InT, 16, (kComplexIn ? 2 : 4), 8, 128, MODE>(j, s);
+    // large even D: one output a thread on a polyphase tile (odd padded lane stride, conflict-free
+    // reads), where the runtime-D kernel's lane stride of D samples hits one LDS bank over and over
+    case 20:
+      return launch_poly_default<TapT, InT, 20, 1, 8, 256, MODE>(j, s);
+    case 24:
+      return launch_poly_default<TapT, InT, 24, 1, 8, 256, MODE>(j, s);
+    case 32:
+      return launch_poly_default<TapT, InT, 32, 1, 8, (kComplexIn ? 128 : 256), MODE>(j, s);
+    case 40:
+      return launch_poly_default<TapT, InT, 40, 1, 8, (kComplexIn ? 128 : 256), MODE>(j, s);
+    case 48:
+      return launch_poly_default<TapT, InT, 48, 1, 8, 128, MODE>(j, s);
+    case 64:
+      return launch_poly_default<TapT, InT, 64, 1, 8, (kComplexIn ? 64 : 128), MODE>(j, s);
     default:
       return launch_rt<TapT, InT, MODE>(j, s);
   }

@@ -27,7 +27,7 @@ def dev(a, cuda):
 
 @pytest.mark.parametrize("n0", [0, 987654321, (1 << 32) + 5])
 @pytest.mark.parametrize("T", [1, 31, 127])
-@pytest.mark.parametrize("D", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 12, 13, 16, 24])
+@pytest.mark.parametrize("D", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 12, 13, 16, 20, 24, 32, 40, 50, 64])
 def test_fm_demod_parity(cuda, D, T, n0):
     from gsdr_amd import ops
     from gsdr_amd.signals import fm_test_signal, lowpass_taps
@@ -43,7 +43,7 @@ def test_fm_demod_parity(cuda, D, T, n0):
 
 @pytest.mark.parametrize("n0", [0, (1 << 32) + 5])
 @pytest.mark.parametrize("T", [1, 31, 127])
-@pytest.mark.parametrize("D", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 12, 13, 16, 24])
+@pytest.mark.parametrize("D", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 12, 13, 16, 20, 24, 32, 40, 50, 64])
 def test_am_demod_parity(cuda, D, T, n0):
     from gsdr_amd import ops
     from gsdr_amd.signals import lowpass_taps, uniform_iq

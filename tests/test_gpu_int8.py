@@ -51,7 +51,7 @@ def test_conversion_exhaustive_through_the_fir(cuda):
     assert y.tobytes() == want.tobytes()
 
 
-@pytest.mark.parametrize("D", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 12, 13, 16, 24])
+@pytest.mark.parametrize("D", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 12, 13, 16, 20, 24, 32, 40, 50, 64])
 @pytest.mark.parametrize("T", [1, 8, 63, 127, 200])
 def test_fir_int8_parity(cuda, D, T):
     from gsdr_amd import ops
@@ -83,7 +83,7 @@ def test_fir_int8_unaligned(cuda, offset_bytes):
     assert normwise_err(y, o.fir(taps, xf, D, n), bound(taps, xf, D, n)) <= FLOAT_TOL
 
 
-@pytest.mark.parametrize("D", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 12, 13, 16, 24])
+@pytest.mark.parametrize("D", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 12, 13, 16, 20, 24, 32, 40, 50, 64])
 def test_fm_am_int8_chains(cuda, D):
     from gsdr_amd import ops
     from gsdr_amd.signals import fm_test_signal

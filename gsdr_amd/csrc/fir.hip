@@ -1,41 +1,15 @@
-// gsdr-mi355x: gsdrFirFC / gsdrFirFF / gsdrFirCC / gsdrFirCF (reference src/fir.cu:73-171,
-// include/gsdr/fir.h:30-68) and the kernel dispatch shared with the FM / AM chains.
+// gsdr-mi355x: gsdrFirFC (reference src/fir.cu:73-171, include/gsdr/fir.h:30-68), its tuning variants
+// and probes. FF / CC / CF and the int8 front end live in fir_ff.hip, fir_cc.hip, fir_cf.hip and
+// fir_int8.hip (one sample-type pair per translation unit, built in parallel).
 #include <hip/hip_runtime.h>
 
 #include "fir_dispatch.hpp"
+#include "fir_entry.hpp"
 #include "gsdr/fir.h"
 #include "gsdr/gsdr_ext.h"
 #include "launch.hpp"
 
 namespace gsdr {
-
-template <class TapT, class InT>
-static hipError_t fir_entry(size_t decimation, const TapT* taps, size_t tapCount, const InT* input,
-                            typename Product<TapT, InT>::type* output, size_t numOutputs, int32_t device,
-                            hipStream_t stream, int variant) {
-  using OutT = typename Product<TapT, InT>::type;
-  if (numOutputs == 0) return hipSuccess;
-  if (decimation == 0 || output == nullptr) return hipErrorInvalidValue;
-  GSDR_ON_DEVICE(device, ([&]() -> hipError_t {
-                   if (tapCount == 0) {
-                     // reference: the tap loop never runs, every output is zero<OUT_T>() (fir.cu:43-46)
-                     const hipError_t st = hipMemsetAsync(output, 0, numOutputs * sizeof(OutT), stream);
-                     return st != hipSuccess ? st : launch_status();
-                   }
-                   if (taps == nullptr || input == nullptr) return hipErrorInvalidValue;
-                   FirJob job;
-                   job.in = input;
-                   job.taps = taps;
-                   job.out = output;
-                   job.D = decimation;
-                   job.T = tapCount;
-                   job.N = numOutputs;
-                   job.L = (numOutputs - 1) * decimation + tapCount;
-                   job.mode = kModeFir;
-                   job.variant = variant;
-                   return launch_fir<TapT, InT, kModeFir>(job, stream);
-                 })());
-}
 
 // Streaming ceiling probe for this traffic mix: reads the 8*N_in input bytes with fully coalesced
 // 16-byte loads and writes 8*N_out bytes (outputs are a sum of loaded samples, not a FIR).
@@ -105,39 +79,6 @@ GSDR_C_LINKAGE hipError_t gsdrFirFC(size_t decimation, const float* taps, size_t
                                     const hipFloatComplex* input, hipFloatComplex* output, size_t numOutputs,
                                     int32_t cudaDevice, hipStream_t cudaStream) GSDR_NO_EXCEPT {
   return fir_entry<float, float2>(decimation, taps, tapCount, input, output, numOutputs, cudaDevice, cudaStream, -1);
-}
-
-GSDR_C_LINKAGE hipError_t gsdrxFirFCInt8(size_t decimation, const float* taps, size_t tapCount, const int8_t* input,
-                                         hipFloatComplex* output, size_t numOutputs, int32_t cudaDevice,
-                                         hipStream_t cudaStream) GSDR_NO_EXCEPT {
-  return fir_entry<float, gsdr::Iq8>(decimation, taps, tapCount, reinterpret_cast<const gsdr::Iq8*>(input), output,
-                                     numOutputs, cudaDevice, cudaStream, -1);
-}
-
-GSDR_C_LINKAGE hipError_t gsdrxFirFCInt8Variant(int variant, size_t decimation, const float* taps, size_t tapCount,
-                                                const int8_t* input, hipFloatComplex* output, size_t numOutputs,
-                                                int32_t cudaDevice, hipStream_t cudaStream) GSDR_NO_EXCEPT {
-  return fir_entry<float, gsdr::Iq8>(decimation, taps, tapCount, reinterpret_cast<const gsdr::Iq8*>(input), output,
-                                     numOutputs, cudaDevice, cudaStream, variant < 0 ? -1 : variant);
-}
-
-GSDR_C_LINKAGE hipError_t gsdrFirFF(size_t decimation, const float* taps, size_t tapCount, const float* input,
-                                    float* output, size_t numOutputs, int32_t cudaDevice,
-                                    hipStream_t cudaStream) GSDR_NO_EXCEPT {
-  return fir_entry<float, float>(decimation, taps, tapCount, input, output, numOutputs, cudaDevice, cudaStream, -1);
-}
-
-GSDR_C_LINKAGE hipError_t gsdrFirCC(size_t decimation, const hipFloatComplex* taps, size_t tapCount,
-                                    const hipFloatComplex* input, hipFloatComplex* output, size_t numOutputs,
-                                    int32_t cudaDevice, hipStream_t cudaStream) GSDR_NO_EXCEPT {
-  return fir_entry<float2, float2>(decimation, taps, tapCount, input, output, numOutputs, cudaDevice, cudaStream,
-                                   -1);
-}
-
-GSDR_C_LINKAGE hipError_t gsdrFirCF(size_t decimation, const hipFloatComplex* taps, size_t tapCount,
-                                    const float* input, hipFloatComplex* output, size_t numOutputs,
-                                    int32_t cudaDevice, hipStream_t cudaStream) GSDR_NO_EXCEPT {
-  return fir_entry<float2, float>(decimation, taps, tapCount, input, output, numOutputs, cudaDevice, cudaStream, -1);
 }
 
 GSDR_C_LINKAGE hipError_t gsdrxFirFCVariant(int variant, size_t decimation, const float* taps, size_t tapCount,

@@ -216,10 +216,12 @@ def test_fir_linearity(cuda):
 
 
 @pytest.mark.parametrize("tt", ["FC", "FF", "CC", "CF"])
-@pytest.mark.parametrize("D,T", [(4, 1001), (4, 4001), (4, 6000), (2, 2500), (8, 3001), (1, 2048)])
+@pytest.mark.parametrize("D,T", [(4, 1001), (4, 4001), (4, 6000), (2, 2500), (8, 3001), (1, 2048), (3, 1500),
+                                 (9, 1500), (50, 4000), (32, 3000), (13, 9000)])
 def test_fir_long_filters(cuda, tt, D, T):
     """Long filters: the polyphase tile grows with the tap span until it leaves the 64 KB LDS budget
-    (near T = 4000 at D = 4), after which the generic kernel runs; both sides of that boundary."""
+    (near T = 4000 at D = 4), after which the generic kernel runs; both sides of that boundary. The
+    runtime-decimation tile (D = 9, 13, 50) narrows to 128 or 64 outputs before giving up."""
     N = 3000 + D
     taps, x = make(tt, T, (N - 1) * D + T, T + D)
     y = run_fir(cuda, taps, x, D, N)

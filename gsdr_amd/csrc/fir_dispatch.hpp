@@ -56,6 +56,15 @@ inline FirParams make_params(const FirJob& j) {
   return p;
 }
 
+// FM tiles overlap by one FIR output (the discriminator pairs y[m] with y[m + 1]). With odd D that
+// stride would put every other tile off the staging alignment (and all of them on the per-sample load
+// path), so those tiles overlap by two outputs instead.
+template <class InT>
+inline uint32_t fm_tile_stride(uint32_t kt, size_t D) {
+  constexpr uint64_t A = SampleT<InT>::kSrcAlign;
+  return ((uint64_t)(kt - 1) * D * sizeof(InT)) % A == 0 ? kt - 1 : kt - 2;
+}
+
 template <class TapT, class InT, int MODE>
 hipError_t launch_generic(const FirJob& j, hipStream_t s) {
   FirParams p = make_params(j);
@@ -77,7 +86,7 @@ hipError_t launch_poly(const FirJob& j, hipStream_t s) {
   const size_t lds = poly_lds_bytes<InT, D, R, WG>((uint32_t)span, MODE);
   if (lds > kMaxTileLds) return launch_generic<TapT, InT, MODE>(j, s);
   p.nch = (uint32_t)nch;
-  const uint32_t stride = (MODE == kModeFm) ? Geo::KT - 1 : Geo::KT;
+  const uint32_t stride = (MODE == kModeFm) ? fm_tile_stride<InT>(Geo::KT, j.D) : Geo::KT;
   p.tile_stride = stride;
   const uint64_t tiles = ceil_div<uint64_t>(j.N, stride);
   if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
@@ -119,7 +128,7 @@ hipError_t launch_contig(const FirJob& j, hipStream_t s) {
   const size_t lds = poly_lds_bytes<InT, D, R, WG>((uint32_t)span, MODE);
   if (lds > kMaxTileLds) return launch_generic<TapT, InT, MODE>(j, s);
   p.nch = (uint32_t)nch;
-  const uint32_t stride = (MODE == kModeFm) ? Geo::KT - 1 : Geo::KT;
+  const uint32_t stride = (MODE == kModeFm) ? fm_tile_stride<InT>(Geo::KT, j.D) : Geo::KT;
   p.tile_stride = stride;
   const uint64_t tiles = ceil_div<uint64_t>(j.N, stride);
   if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
@@ -201,7 +210,7 @@ hipError_t launch_multi(const FirJob& j, const MultiParams& mp, hipStream_t s) {
   const size_t lds = poly_lds_bytes<InT, D, R, WG>((uint32_t)span, MODE);
   if (lds > kMaxTileLds) return hipErrorNotSupported;
   p.nch = (uint32_t)nch;
-  const uint32_t stride = (MODE == kModeFm) ? Geo::KT - 1 : Geo::KT;
+  const uint32_t stride = (MODE == kModeFm) ? fm_tile_stride<InT>(Geo::KT, j.D) : Geo::KT;
   p.tile_stride = stride;
   const uint64_t tiles = ceil_div<uint64_t>(j.N, stride);
   if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
@@ -279,7 +288,7 @@ hipError_t launch_rt_wg(const FirJob& j, uint32_t nch, size_t lds, hipStream_t s
   constexpr int IC = 16;
   FirParams p = make_params(j);
   p.nch = nch;
-  const uint32_t stride = (MODE == kModeFm) ? WG - 1 : WG;
+  const uint32_t stride = (MODE == kModeFm) ? fm_tile_stride<InT>(WG, j.D) : WG;
   p.tile_stride = stride;
   const uint64_t tiles = ceil_div<uint64_t>(j.N, stride);
   if (tiles > 0x7fffffffull) return hipErrorInvalidValue;

@@ -564,7 +564,8 @@ __device__ __forceinline__ void tile_epilogue(const FirParams& p, uint64_t out0,
       if (m < p.N) out[m] = am_env(acc[r]);
     }
   } else {
-    // Tiles overlap by one FIR output; the neighbour's first output comes through LDS.
+    // Tiles overlap by one or two FIR outputs (tile_stride = KT - 1 or KT - 2, fm_tile_stride); the
+    // neighbouring thread's first output comes through LDS.
     xs[t] = acc[0];
     __syncthreads();
     const float2 nxt = (t + 1 < WG) ? xs[t + 1] : acc[R - 1];
@@ -574,7 +575,7 @@ __device__ __forceinline__ void tile_epilogue(const FirParams& p, uint64_t out0,
       const float2 y1 = (r + 1 < R) ? acc[r + 1] : nxt;
       const uint32_t ml = local0 + r;
       const uint64_t m = out0 + ml;
-      if (ml < (uint32_t)(WG * R - 1) && m < p.N) out[m] = fm_disc(acc[r], y1, p.fm_gain);
+      if (ml < p.tile_stride && m < p.N) out[m] = fm_disc(acc[r], y1, p.fm_gain);
     }
   }
 }

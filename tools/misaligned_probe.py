@@ -1,9 +1,14 @@
 """Time gsdrFirFC (D = 4, T = 127, 2^26 samples) with the input pointer offset by 0, 1 and 2 complex samples
 (16-, 8- and 16-byte aligned) -- the cost of the per-sample staging path (development tool)."""
-import os, sys, torch
-sys.path.insert(0, '/root/repo')
-from gsdr_amd import abi
-from gsdr_amd.signals import lowpass_taps
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from gsdr_amd import abi  # noqa: E402
+from gsdr_amd.signals import lowpass_taps  # noqa: E402
+
 dev = torch.device('cuda', 0)
 n_in, T, D = (1 << 26) + 8, 127, 4
 x = (torch.rand(2 * n_in, device=dev) * 2 - 1).view(torch.complex64)

@@ -65,6 +65,17 @@ inline uint32_t fm_tile_stride(uint32_t kt, size_t D) {
   return ((uint64_t)(kt - 1) * D * sizeof(InT)) % A == 0 ? kt - 1 : kt - 2;
 }
 
+// Complex input 8 bytes off 16-byte alignment, with every tile start equally off (even samples per
+// tile stride): the tiled kernels stage it with shifted 16-byte loads (stage_tile's SH mode).
+template <class InT>
+inline bool shifted_staging(const void* in, uint64_t samples_per_tile) {
+  if constexpr (std::is_same<InT, float2>::value) {
+    return (reinterpret_cast<uintptr_t>(in) % 16) == 8 && samples_per_tile % 2 == 0;
+  } else {
+    return false;
+  }
+}
+
 template <class TapT, class InT, int MODE>
 hipError_t launch_generic(const FirJob& j, hipStream_t s) {
   FirParams p = make_params(j);
@@ -94,6 +105,11 @@ hipError_t launch_poly(const FirJob& j, hipStream_t s) {
   const bool vec = (reinterpret_cast<uintptr_t>(j.in) % A) == 0 && ((uint64_t)stride * D * sizeof(InT)) % A == 0;
   if (vec) {
     k_fir_poly<TapT, InT, D, R, JC, WG, true, MODE, ABL, NT, XM, CST, DMA><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
+  } else if (shifted_staging<InT>(j.in, (uint64_t)stride * D)) {
+    if constexpr (std::is_same<InT, float2>::value) {
+      k_fir_poly<TapT, InT, D, R, JC, WG, false, MODE, ABL, NT, XM, CST, false, true>
+          <<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
+    }
   } else {
     k_fir_poly<TapT, InT, D, R, JC, WG, false, MODE, ABL, NT, XM, CST, DMA><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
   }
@@ -135,6 +151,10 @@ hipError_t launch_contig(const FirJob& j, hipStream_t s) {
   const bool vec = aligned16(j.in) && ((uint64_t)stride * D * sizeof(InT)) % 16 == 0;
   if (vec) {
     k_fir_contig<TapT, InT, D, R, IC, WG, true, MODE><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
+  } else if (shifted_staging<InT>(j.in, (uint64_t)stride * D)) {
+    if constexpr (std::is_same<InT, float2>::value) {
+      k_fir_contig<TapT, InT, D, R, IC, WG, false, MODE, true><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
+    }
   } else {
     k_fir_contig<TapT, InT, D, R, IC, WG, false, MODE><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
   }

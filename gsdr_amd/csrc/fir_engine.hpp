@@ -371,7 +371,12 @@ __device__ __forceinline__ bool stage_body_dma(float4* __restrict__ lds, const I
   }
 }
 
-template <class InT, class Geo, int WG, bool VEC, int MODE, bool NT = false, bool DMA = false>
+// SH (complex samples only): the input is 8 bytes off 16-byte alignment at every tile start. The tile
+// body is then loaded as aligned 16-byte granules starting one sample early, and each loaded pair is
+// split over two LDS granules (second half of slot g - 1, first half of slot g); the halo re-writes the
+// body's last slot whole. The NCO phasor is a function of the absolute index, so the odd-start pairs
+// mix exactly as the even-start ones would.
+template <class InT, class Geo, int WG, bool VEC, int MODE, bool NT = false, bool DMA = false, bool SH = false>
 __device__ __forceinline__ void stage_tile(float4* __restrict__ lds, const InT* __restrict__ in, uint64_t S0,
                                            uint32_t NG, const FirParams& p) {
   constexpr int G = Geo::G;
@@ -385,6 +390,39 @@ __device__ __forceinline__ void stage_tile(float4* __restrict__ lds, const InT* 
   const PhaseWalk pw = phase_walk<G, WG>(p.nco_n0, S0, p.nco_inc);
   // wave-uniform: is the whole staged span readable? (every tile but the last)
   const bool whole = VEC && (S0 + (uint64_t)NG * G <= p.L);
+  if constexpr (SH) {
+    static_assert(std::is_same<InT, float2>::value && !VEC, "shifted staging is for 8-byte-aligned complex input");
+    if (S0 + (uint64_t)NG * G <= p.L) {
+      const float4* __restrict__ src = reinterpret_cast<const float4*>(in + S0 - 1);  // 16-byte aligned
+      float2* __restrict__ l2 = reinterpret_cast<float2*>(lds);
+#pragma unroll
+      for (int b0 = 0; b0 < BPT; b0 += SB) {
+        float4 v[SB];
+#pragma unroll
+        for (int k = 0; k < SB; ++k) {
+          if constexpr (NT) {
+            v[k] = load16_nt(src + (b0 + k) * WG + tid);
+          } else {
+            v[k] = src[(b0 + k) * WG + tid];
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < SB; ++k) {
+          const uint32_t g = (b0 + k) * WG + tid;
+          // samples S0 + 2g - 1 (odd start relative to the tile) and S0 + 2g
+          const float4 w = stage_transform_ph<InT, MODE>(v[k], pw.ph0 + (uint32_t)(b0 + k) * pw.step - pw.inc, !pw.odd,
+                                                         pw.inc);
+          if (g > 0) l2[2 * Geo::padded(g - 1) + 1] = make_float2(w.x, w.y);
+          l2[2 * Geo::padded(g)] = make_float2(w.z, w.w);
+        }
+      }
+      for (uint32_t g = BPT * WG - 1 + tid; g < NG; g += WG) {
+        const uint64_t s = S0 + (uint64_t)g * G;
+        lds[Geo::padded(g)] = stage_transform<InT, MODE>(load_granule<InT, false>(in, s, p.L), (uint32_t)s, p);
+      }
+      return;
+    }
+  }
   if constexpr (DMA) {
     if (whole && stage_body_dma<InT, Geo, WG, MODE, NT>(lds, in, S0)) {
       for (uint32_t g = BPT * WG + tid; g < NG; g += WG) {
@@ -645,7 +683,7 @@ __device__ __forceinline__ uint32_t tile_of_block() {
 }
 
 template <class TapT, class InT, int D, int R, int JC, int WG, bool VEC, int MODE, int ABL = 0, bool NT = false,
-          bool XM = false, int CST = 0, bool DMA = false>
+          bool XM = false, int CST = 0, bool DMA = false, bool SH = false>
 __global__ __launch_bounds__(WG) void k_fir_poly(FirParams p) {
   using Geo = TileGeo<InT, D, R, WG>;
   using OutT = typename Product<TapT, InT>::type;
@@ -659,7 +697,7 @@ __global__ __launch_bounds__(WG) void k_fir_poly(FirParams p) {
   const uint32_t span = p.nch * JC * D;
   const uint32_t NG = ((Geo::KT - 1) * D + span + G - 1) / G;
   // LDS: [tile granules | FM exchange (WG float2)]
-  if constexpr (ABL != 2) stage_tile<InT, Geo, WG, VEC, MODE, NT, DMA>(lds, in, S0, NG, p);
+  if constexpr (ABL != 2) stage_tile<InT, Geo, WG, VEC, MODE, NT, DMA, SH>(lds, in, S0, NG, p);
   __syncthreads();
 
   OutT acc[R];
@@ -767,7 +805,7 @@ __global__ __launch_bounds__(WG) void k_fir_multi(FirParams p, MultiParams mp) {
 // Kernel 2: contiguous-window kernel for small D (D = 1 in particular).
 //   IC = taps per chunk (a multiple of R*D).
 // ------------------------------------------------------------------------------------------------
-template <class TapT, class InT, int D, int R, int IC, int WG, bool VEC, int MODE>
+template <class TapT, class InT, int D, int R, int IC, int WG, bool VEC, int MODE, bool SH = false>
 __global__ __launch_bounds__(WG) void k_fir_contig(FirParams p) {
   using Geo = TileGeo<InT, D, R, WG>;
   using OutT = typename Product<TapT, InT>::type;
@@ -784,7 +822,7 @@ __global__ __launch_bounds__(WG) void k_fir_contig(FirParams p) {
   const uint32_t span = p.nch * IC;
   const uint32_t NG = ((Geo::KT - 1) * D + span + G - 1) / G;
 
-  stage_tile<InT, Geo, WG, VEC, MODE>(lds, in, S0, NG, p);
+  stage_tile<InT, Geo, WG, VEC, MODE, false, false, SH>(lds, in, S0, NG, p);
   __syncthreads();
 
   OutT acc[R];

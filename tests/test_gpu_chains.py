@@ -63,14 +63,16 @@ def test_nco_against_golden_increment(cuda):
     assert ops.nco_phase_increment(FS, TUNE, CHAN) == o.nco_inc(FS, TUNE, CHAN)
 
 
-def test_fm_streaming_chunks_equal_monolithic(cuda):
+@pytest.mark.parametrize("D", [4, 1, 3, 5])
+def test_fm_streaming_chunks_equal_monolithic(cuda, D):
     """Streaming contract (fm.h:26, firstSampleIndex fm.h:48): K chunked calls with numLowPassTaps of
     overlap reproduce one call bit for bit -- the NCO phase is a function of the absolute index and
-    each FIR output is computed by the same arithmetic wherever its tile falls."""
+    each FIR output is computed by the same arithmetic wherever its tile falls. Odd D puts chunks at
+    8-byte-aligned addresses (shifted staging, odd-start NCO pairs)."""
     from gsdr_amd import ops
     from gsdr_amd.signals import fm_test_signal, lowpass_taps
 
-    D, T, N = 4, 127, 30000
+    T, N = 127, 30000
     x = dev(fm_test_signal(N * D + T, fs=FS, seed=3), cuda)
     taps = dev(lowpass_taps(T, 0.1), cuda)
     whole = ops.fm_demod(x, taps, FS, TUNE, CHAN, DEV, D, 1000, N)

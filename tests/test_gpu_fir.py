@@ -227,3 +227,15 @@ def test_fir_long_filters(cuda, tt, D, T):
     y = run_fir(cuda, taps, x, D, N)
     ref = o.fir(taps, x, D, N)
     assert normwise_err(y, ref, bound(taps, x, D, N)) <= FLOAT_TOL
+
+
+@pytest.mark.parametrize("tt,D", [("FC", 4), ("FC", 1), ("CC", 2), ("FC", 3), ("FC", 8), ("CC", 16), ("FC", 32)])
+def test_fir_shifted_staging_bit_identical(cuda, tt, D):
+    """A complex input 8 bytes off 16-byte alignment is staged with shifted 16-byte loads (stage_tile
+    SH mode); the outputs must equal those of the same samples at an aligned address, bit for bit."""
+    N, T = 3 * 4096 + 5, 127
+    L = (N - 1) * D + T
+    taps, x = make(tt, T, L, seed=91 + D)
+    aligned = run_fir(cuda, taps, x, D, N)
+    shifted = run_fir(cuda, taps, x, D, N, x_offset=1)
+    assert aligned.tobytes() == shifted.tobytes()

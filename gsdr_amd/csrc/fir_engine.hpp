@@ -606,7 +606,10 @@ __device__ __forceinline__ void tile_epilogue(const FirParams& p, uint64_t out0,
     // neighbouring thread's first output comes through LDS.
     xs[t] = acc[0];
     __syncthreads();
-    const float2 nxt = (t + 1 < WG) ? xs[t + 1] : acc[R - 1];
+    // value select (both loads in range): a select of the two addresses became a flat load through
+    // scratch when R = 1
+    const float2 nb = xs[t + 1 < WG ? t + 1 : t];
+    const float2 nxt = (t + 1 < WG) ? nb : acc[R - 1];
     float* out = reinterpret_cast<float*>(p.out);
 #pragma unroll
     for (int r = 0; r < R; ++r) {

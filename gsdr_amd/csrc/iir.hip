@@ -114,20 +114,25 @@ __device__ __forceinline__ void mat_mul(const double* __restrict__ A, const doub
 // else the global table itself): T[h] = T[h/2]^2, then T[h + q] = T[h] T[q].
 // barrier for the setup workgroup; the device-scope fence is needed only when the table lives in
 // global memory (it costs ~1 us, and the doubling rounds need ~50 barriers)
-__device__ __forceinline__ void sync_table(const double* work) {
-  if (!work) __threadfence();
+template <bool INLDS>
+__device__ __forceinline__ void sync_table() {
+  if constexpr (!INLDS) __threadfence();
   __syncthreads();
 }
 
-template <class S, int P, int NT>
-__device__ void iir_setup(const Coeffs& cf, const S* __restrict__ yh, typename Acc<S>::type* __restrict__ s0,
-                          double* __restrict__ T, int levels, double* __restrict__ work) {
+// INLDS (compile time): `work` is the caller's LDS table. Inlined with a compile-time choice, the table
+// accesses compile to ds_read / ds_write; a runtime select between LDS and global made every one of
+// them a flat access.
+template <class S, int P, int NT, bool INLDS>
+__device__ __forceinline__ void iir_setup(const Coeffs& cf, const S* __restrict__ yh,
+                                          typename Acc<S>::type* __restrict__ s0, double* __restrict__ T, int levels,
+                                          double* __restrict__ work) {
   const int t = threadIdx.x;
   const int Pk = cf.K - 1;
   constexpr int PP = P * P;
   if (t < P) s0[t] = (yh && t < Pk) ? to_acc(yh[t]) : zero_s(typename Acc<S>::type{});
   for (int lv = 0; lv <= levels; ++lv) {
-    double* __restrict__ W = work ? work : T + (size_t)lv * kGroup * PP;
+    double* __restrict__ W = INLDS ? work : T + (size_t)lv * kGroup * PP;
     if (lv == 0) {
       if (t < P) {  // M_0, column t
         double am[P + 1];
@@ -148,7 +153,7 @@ __device__ void iir_setup(const Coeffs& cf, const S* __restrict__ yh, typename A
         for (int i = 0; i < P; ++i) W[PP + i * P + t] = ys[i];
       }
     } else {  // M_lv = M_{lv-1}^64 = (M_{lv-1}^32)^2, from the previous level's table
-      const double* Tp = work ? work : T + (size_t)(lv - 1) * kGroup * PP;
+      const double* Tp = INLDS ? work : T + (size_t)(lv - 1) * kGroup * PP;
       double m2[(PP + NT - 1) / NT];
       int c = 0;
       for (int e = t; e < PP; e += NT, ++c) {
@@ -158,15 +163,15 @@ __device__ void iir_setup(const Coeffs& cf, const S* __restrict__ yh, typename A
         for (int l = 0; l < P; ++l) acc = fma(Tp[32 * PP + i * P + l], Tp[32 * PP + l * P + j], acc);
         m2[c] = acc;
       }
-      sync_table(work);
+      sync_table<INLDS>();
       c = 0;
       for (int e = t; e < PP; e += NT, ++c) W[PP + e] = m2[c];
     }
     for (int e = t; e < PP; e += NT) W[e] = (e / P == e % P) ? 1.0 : 0.0;
-    sync_table(work);
+    sync_table<INLDS>();
     for (int h = 2; h < kGroup; h *= 2) {
       mat_mul<P>(W + (h / 2) * PP, W + (h / 2) * PP, W + h * PP, t, NT);
-      sync_table(work);
+      sync_table<INLDS>();
       for (int w = t; w < (h - 1) * PP; w += NT) {
         const int q = 1 + w / PP, e = w % PP;
         if (h + q < kGroup) {
@@ -177,9 +182,9 @@ __device__ void iir_setup(const Coeffs& cf, const S* __restrict__ yh, typename A
           W[(h + q) * PP + e] = acc;
         }
       }
-      sync_table(work);
+      sync_table<INLDS>();
     }
-    if (work) {  // publish the level's table
+    if constexpr (INLDS) {  // publish the level's table
       double* Tl = T + (size_t)lv * kGroup * PP;
       for (int e = t; e < kGroup * PP; e += NT) Tl[e] = W[e];
       __syncthreads();
@@ -283,8 +288,8 @@ __global__ __launch_bounds__(TileShape<S>::WG) void k_iir_chunks(Coeffs cf, cons
   if constexpr (PASS == kTails) {
     // the extra last workgroup builds the scan constants while the others compute the tails
     if (blockIdx.x == gridDim.x - 1) {
-      iir_setup<S, P, TSh::WG>(cf, static_cast<const S*>(setup.yh), static_cast<A*>(setup.s0), setup.T, setup.levels,
-                               kTableInLds<P> ? reinterpret_cast<double*>(smem) : nullptr);
+      iir_setup<S, P, TSh::WG, kTableInLds<P>>(cf, static_cast<const S*>(setup.yh), static_cast<A*>(setup.s0), setup.T,
+                                               setup.levels, reinterpret_cast<double*>(smem));
       return;
     }
   }

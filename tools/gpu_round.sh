@@ -13,6 +13,7 @@ rc=$?; echo "bench exit $rc"; tail -1 gpurun_out/bench.log; [ $rc = 0 ] || exit 
 rm -rf gpurun_out/prof_bench gpurun_out/pmc_bench
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench -- python bench.py > gpurun_out/prof_bench.log 2>&1
 rc=$?; echo "rocprof bench exit $rc"; [ $rc = 0 ] || exit $rc
+grep kernel_us_mean gpurun_out/prof_bench.log | tail -1 > gpurun_out/bench_profiled.json  # the profiled run's own line
 bash tools/pmc.sh pmc_bench python bench.py --steps 3 --warmup 1 --no-secondary --no-cpu-baseline > gpurun_out/pmc_bench.log 2>&1
 rc=$?; echo "pmc exit $rc"; tail -25 gpurun_out/pmc_bench.log
 exit $rc

@@ -38,6 +38,9 @@ if stats:
             f.write(f"# {fir_name}: per-dispatch duration (us) from rocprofv3 --kernel-trace of `python bench.py`\n")
             f.write(f"# dispatches {len(d)}; mean of the last {a.steps} (the timed steps) = {timed_mean:.2f} us\n")
             f.write("\n".join(f"{x:.2f}" for x in d) + "\n")
+prof_line = os.path.join(ROOT, "gpurun_out", "bench_profiled.json")
+if os.path.exists(prof_line):  # the profiled run's own bench line (gpu_round.sh), to set beside the trace
+    shutil.copy(prof_line, os.path.join(prof, f"{a.tag}_bench_line_profiled.json"))
 summ = json.load(open(os.path.join(ROOT, a.pmc_dir, "summary.json")))
 shutil.copy(os.path.join(ROOT, a.pmc_dir, "summary.json"), os.path.join(prof, f"{a.tag}_pmc_summary.json"))
 k = summ[a.kernel]

@@ -15,7 +15,7 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ap = argparse.ArgumentParser()
 ap.add_argument("tag")
-ap.add_argument("--kernel", default="void k_fir_poly<float, f2, 4, 4, 16, 256, true, 0, 0, true, false, 0, false>")
+ap.add_argument("--kernel", default="void k_fir_poly<float, f2, 4, 4, 16, 256, true, 0, 0, true, false, 0, false, false>")
 ap.add_argument("--stats-dir", default="gpurun_out/prof_bench")
 ap.add_argument("--pmc-dir", default="gpurun_out/pmc_bench")
 ap.add_argument("--steps", type=int, default=100, help="timed steps of the profiled bench run")

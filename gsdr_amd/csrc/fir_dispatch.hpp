@@ -65,12 +65,16 @@ inline uint32_t fm_tile_stride(uint32_t kt, size_t D) {
   return ((uint64_t)(kt - 1) * D * sizeof(InT)) % A == 0 ? kt - 1 : kt - 2;
 }
 
-// Complex input 8 bytes off 16-byte alignment, with every tile start equally off (even samples per
-// tile stride): the tiled kernels stage it with shifted 16-byte loads (stage_tile's SH mode).
+// Complex input 8 bytes off 16-byte alignment, or int8 I/Q 2 bytes off 4-byte alignment, with every tile
+// start equally off (even samples per tile stride): the tiled kernels stage it with shifted aligned
+// loads (stage_tile's SH mode).
 template <class InT>
 inline bool shifted_staging(const void* in, uint64_t samples_per_tile) {
   if constexpr (std::is_same<InT, float2>::value) {
     return (reinterpret_cast<uintptr_t>(in) % 16) == 8 && samples_per_tile % 2 == 0;
+  } else if constexpr (std::is_same<InT, Iq8>::value) {
+    // int8 I/Q one sample (2 bytes) off 4-byte alignment: shifted 4-byte word loads
+    return (reinterpret_cast<uintptr_t>(in) % 4) == 2 && samples_per_tile % 2 == 0;
   } else {
     return false;
   }
@@ -106,7 +110,7 @@ hipError_t launch_poly(const FirJob& j, hipStream_t s) {
   if (vec) {
     k_fir_poly<TapT, InT, D, R, JC, WG, true, MODE, ABL, NT, XM, CST, DMA><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
   } else if (shifted_staging<InT>(j.in, (uint64_t)stride * D)) {
-    if constexpr (std::is_same<InT, float2>::value) {
+    if constexpr (std::is_same<InT, float2>::value || std::is_same<InT, Iq8>::value) {
       k_fir_poly<TapT, InT, D, R, JC, WG, false, MODE, ABL, NT, XM, CST, false, true>
           <<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
     }
@@ -152,7 +156,7 @@ hipError_t launch_contig(const FirJob& j, hipStream_t s) {
   if (vec) {
     k_fir_contig<TapT, InT, D, R, IC, WG, true, MODE><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
   } else if (shifted_staging<InT>(j.in, (uint64_t)stride * D)) {
-    if constexpr (std::is_same<InT, float2>::value) {
+    if constexpr (std::is_same<InT, float2>::value || std::is_same<InT, Iq8>::value) {
       k_fir_contig<TapT, InT, D, R, IC, WG, false, MODE, true><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
     }
   } else {

@@ -371,7 +371,8 @@ __device__ __forceinline__ bool stage_body_dma(float4* __restrict__ lds, const I
   }
 }
 
-// SH (complex samples only): the input is 8 bytes off 16-byte alignment at every tile start. The tile
+// SH (complex or int8 I/Q samples): the input is one sample off its aligned granule load (complex: 8 bytes
+// off 16; int8 I/Q: 2 bytes off 4) at every tile start. The tile
 // body is then loaded as aligned 16-byte granules starting one sample early, and each loaded pair is
 // split over two LDS granules (second half of slot g - 1, first half of slot g); the halo re-writes the
 // body's last slot whole. The NCO phasor is a function of the absolute index, so the odd-start pairs
@@ -391,19 +392,31 @@ __device__ __forceinline__ void stage_tile(float4* __restrict__ lds, const InT* 
   // wave-uniform: is the whole staged span readable? (every tile but the last)
   const bool whole = VEC && (S0 + (uint64_t)NG * G <= p.L);
   if constexpr (SH) {
-    static_assert(std::is_same<InT, float2>::value && !VEC, "shifted staging is for 8-byte-aligned complex input");
+    static_assert((std::is_same<InT, float2>::value || std::is_same<InT, Iq8>::value) && !VEC,
+                  "shifted staging is for 8-byte-aligned complex or 2-byte-aligned int8 I/Q input");
     if (S0 + (uint64_t)NG * G <= p.L) {
-      const float4* __restrict__ src = reinterpret_cast<const float4*>(in + S0 - 1);  // 16-byte aligned
       float2* __restrict__ l2 = reinterpret_cast<float2*>(lds);
 #pragma unroll
       for (int b0 = 0; b0 < BPT; b0 += SB) {
         float4 v[SB];
+        if constexpr (std::is_same<InT, Iq8>::value) {
+          const uint32_t* __restrict__ src = reinterpret_cast<const uint32_t*>(in + S0 - 1);  // 4-byte aligned
+          uint32_t w[SB];
 #pragma unroll
-        for (int k = 0; k < SB; ++k) {
-          if constexpr (NT) {
-            v[k] = load16_nt(src + (b0 + k) * WG + tid);
-          } else {
-            v[k] = src[(b0 + k) * WG + tid];
+          for (int k = 0; k < SB; ++k) {
+            w[k] = NT ? __builtin_nontemporal_load(src + (b0 + k) * WG + tid) : src[(b0 + k) * WG + tid];
+          }
+#pragma unroll
+          for (int k = 0; k < SB; ++k) v[k] = iq8x2_granule(w[k]);
+        } else {
+          const float4* __restrict__ src = reinterpret_cast<const float4*>(in + S0 - 1);  // 16-byte aligned
+#pragma unroll
+          for (int k = 0; k < SB; ++k) {
+            if constexpr (NT) {
+              v[k] = load16_nt(src + (b0 + k) * WG + tid);
+            } else {
+              v[k] = src[(b0 + k) * WG + tid];
+            }
           }
         }
 #pragma unroll

@@ -121,3 +121,23 @@ def test_fir_int8_full_config(cuda):
     yf = ops.fir(taps, xf, D, n)
     torch.cuda.synchronize()
     assert torch.equal(y.view(torch.float32), yf.view(torch.float32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("offset_bytes", [2, 6])
+@pytest.mark.parametrize("D", [1, 2, 3, 4, 5, 8, 13])
+def test_fir_int8_shifted_staging_bit_identical(cuda, D, offset_bytes):
+    """Odd-sample (2-byte) offsets take stage_tile's shifted word loads: outputs equal the aligned call's."""
+    import torch
+    from gsdr_amd import ops
+
+    T, n = 127, 60000
+    L = (n - 1) * D + T
+    raw = iq8(L + 8, seed=D)
+    taps = dev(taps_for(T), cuda)
+    buf = dev(raw, cuda)
+    aligned = torch.empty(2 * L + 16, dtype=torch.int8, device=buf.device)[:2 * L]
+    aligned.copy_(buf[offset_bytes:offset_bytes + 2 * L])
+    y0 = host(ops.fir(taps, aligned, D, n))
+    y1 = host(ops.fir(taps, buf[offset_bytes:offset_bytes + 2 * L], D, n))
+    assert y1.tobytes() == y0.tobytes()

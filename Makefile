@@ -13,7 +13,7 @@ SRCS := $(wildcard gsdr_amd/csrc/*.hip)
 HDRS := $(wildcard gsdr_amd/csrc/*.hpp) $(wildcard include/gsdr/*.h)
 OBJS := $(patsubst gsdr_amd/csrc/%.hip,$(BUILD)/%.o,$(SRCS))
 
-all: gsdr_amd/libgsdr.so oracle/build/liboracle.so
+all: gsdr_amd/libgsdr.so oracle/build/liboracle.so examples
 
 $(BUILD)/%.o: gsdr_amd/csrc/%.hip $(HDRS)
 	@mkdir -p $(BUILD)
@@ -21,6 +21,17 @@ $(BUILD)/%.o: gsdr_amd/csrc/%.hip $(HDRS)
 
 gsdr_amd/libgsdr.so: $(OBJS)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -Wl,-rpath,/opt/rocm/lib $(OBJS) -o $@
+
+# Tuning-probe build (ablation variants >= 100 of gsdrxFirFCVariant): the product objects with fir.hip
+# recompiled under GSDR_TUNING_PROBES. Loaded by tools/ through GSDR_LIB; never by the tests or bench.
+probes: $(BUILD)/probes/libgsdr_probes.so
+
+$(BUILD)/probes/fir.o: gsdr_amd/csrc/fir.hip $(HDRS)
+	@mkdir -p $(BUILD)/probes
+	$(HIPCC) $(HIPFLAGS) -DGSDR_TUNING_PROBES -c $< -o $@
+
+$(BUILD)/probes/libgsdr_probes.so: $(filter-out $(BUILD)/fir.o,$(OBJS)) $(BUILD)/probes/fir.o
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -Wl,-rpath,/opt/rocm/lib $^ -o $@
 
 oracle/build/liboracle.so: oracle/gsdr_oracle.c oracle/gsdr_oracle.h
 	@mkdir -p oracle/build
@@ -36,4 +47,4 @@ $(BUILD)/fm_receiver: examples/fm_receiver.cpp gsdr_amd/libgsdr.so $(HDRS)
 clean:
 	rm -rf $(BUILD) gsdr_amd/libgsdr.so oracle/build
 
-.PHONY: all clean examples
+.PHONY: all clean examples probes

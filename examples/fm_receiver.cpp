@@ -1,7 +1,10 @@
 // gsdr-mi355x example: a reference-style C++ host caller of the C ABI (no Python, no torch).
 // Builds an FM test signal on the host, filters/decimates it with gsdrFirFC, demodulates it with the
 // fused gsdrFmDemod in two streaming chunks, and checks the chunks match a single call.
-//   make examples && LD_LIBRARY_PATH=gsdr_amd ./build/fm_receiver
+//   make examples && ./build/fm_receiver [dump_dir]
+// With dump_dir, the taps, the input and the gsdrFirFC / gsdrFmDemod outputs are written there as raw
+// little-endian float32 files (taps.f32, x.c64, fir.c64, fm.f32) for tests/test_gpu_example.py, which
+// checks them against the CPU oracle.
 #include <gsdr/gsdr.h>
 #include <hip/hip_runtime.h>
 
@@ -20,7 +23,16 @@
     }                                                                                 \
   } while (0)
 
-int main() {
+static bool dump(const char* dir, const char* name, const void* data, size_t bytes) {
+  char path[4096];
+  std::snprintf(path, sizeof(path), "%s/%s", dir, name);
+  FILE* f = std::fopen(path, "wb");
+  if (f == nullptr) return false;
+  const bool ok = std::fwrite(data, 1, bytes, f) == bytes;
+  return std::fclose(f) == 0 && ok;
+}
+
+int main(int argc, char** argv) {
   const float fs = 1.0e6f, chan = 1.0e5f, dev = 2.0e4f;
   const uint32_t D = 4;
   const size_t T = 127, N = 1 << 20, L = N * D + T;
@@ -92,11 +104,20 @@ int main() {
   CHECK(gsdrxStreamDestroy(rx));
 
   std::vector<float> fm(N), fm2(N), fm8(N), fm8s(N);
+  std::vector<hipFloatComplex> y(N);
+  CHECK(hipMemcpyAsync(y.data(), dY, N * sizeof(hipFloatComplex), hipMemcpyDeviceToHost, stream));
   CHECK(hipMemcpyAsync(fm.data(), dFm, N * sizeof(float), hipMemcpyDeviceToHost, stream));
   CHECK(hipMemcpyAsync(fm2.data(), dFm2, N * sizeof(float), hipMemcpyDeviceToHost, stream));
   CHECK(hipMemcpyAsync(fm8.data(), dFm8, N * sizeof(float), hipMemcpyDeviceToHost, stream));
   CHECK(hipMemcpyAsync(fm8s.data(), dFm8s, N * sizeof(float), hipMemcpyDeviceToHost, stream));
   CHECK(hipStreamSynchronize(stream));
+  if (argc > 1 && !(dump(argv[1], "taps.f32", taps.data(), T * sizeof(float)) &&
+                    dump(argv[1], "x.c64", x.data(), L * sizeof(hipFloatComplex)) &&
+                    dump(argv[1], "fir.c64", y.data(), N * sizeof(hipFloatComplex)) &&
+                    dump(argv[1], "fm.f32", fm.data(), N * sizeof(float)))) {
+    std::fprintf(stderr, "cannot write to %s\n", argv[1]);
+    return 1;
+  }
   // the stream emits every output whose window has arrived: all N (the input holds N*D + T samples)
   const bool stream_same = produced == N && std::memcmp(fm8.data(), fm8s.data(), N * sizeof(float)) == 0;
 

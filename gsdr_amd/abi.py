@@ -12,7 +12,9 @@ import os
 
 __all__ = ["lib", "LIB_PATH", "SIGNATURES", "GsdrError", "Complex", "check"]
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgsdr.so")
+# GSDR_LIB selects another build of the same ABI (the tools/ scripts load the tuning-probe build,
+# build/probes/libgsdr_probes.so); the default is the in-tree product library.
+LIB_PATH = os.environ.get("GSDR_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgsdr.so")
 
 _p = ctypes.c_void_p
 _sz = ctypes.c_size_t

@@ -11,6 +11,10 @@
 
 namespace gsdr {
 
+#ifdef GSDR_TUNING_PROBES
+// Tuning probes are not part of the product library: they are compiled only into
+// build/probes/libgsdr_probes.so (`make probes`), which the tools/ scripts load through GSDR_LIB.
+
 // Streaming ceiling probe for this traffic mix: reads the 8*N_in input bytes with fully coalesced
 // 16-byte loads and writes 8*N_out bytes (outputs are a sum of loaded samples, not a FIR).
 template <bool NT>
@@ -70,6 +74,9 @@ hipError_t launch_fc_probe(const FirJob& j, hipStream_t s) {
       return hipErrorInvalidValue;
   }
 }
+#else
+hipError_t launch_fc_probe(const FirJob&, hipStream_t) { return hipErrorInvalidValue; }
+#endif  // GSDR_TUNING_PROBES
 
 }  // namespace gsdr
 

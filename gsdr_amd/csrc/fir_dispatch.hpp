@@ -152,7 +152,8 @@ hipError_t launch_contig(const FirJob& j, hipStream_t s) {
   p.tile_stride = stride;
   const uint64_t tiles = ceil_div<uint64_t>(j.N, stride);
   if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
-  const bool vec = aligned16(j.in) && ((uint64_t)stride * D * sizeof(InT)) % 16 == 0;
+  constexpr uint64_t A = SampleT<InT>::kSrcAlign;
+  const bool vec = (reinterpret_cast<uintptr_t>(j.in) % A) == 0 && ((uint64_t)stride * D * sizeof(InT)) % A == 0;
   if (vec) {
     k_fir_contig<TapT, InT, D, R, IC, WG, true, MODE><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
   } else if (shifted_staging<InT>(j.in, (uint64_t)stride * D)) {
@@ -172,9 +173,10 @@ hipError_t launch_contig(const FirJob& j, hipStream_t s) {
 //   10/11 default, tile stored through LDS | 13 matrix-core core (k_fir_mfma_bc, T <= 132)
 //   14 default, tile body staged by LDS-DMA (global_load_lds)
 //   24 WG=64 R=4 | 28 WG=128 R=4
-// Ablation probes (fir.hip): 104 compute only, 105 staging only, 107 staging only (non-temporal),
-// 113 matrix-core compute only, 117 staging only by LDS-DMA,
-// 110/111 streaming ceiling of this traffic mix (plain / non-temporal).
+// Ablation probes (fir.hip, compiled only into the probes library, `make probes`; the product library
+// returns hipErrorInvalidValue for them): 104 compute only, 105 staging only, 107 staging only
+// (non-temporal), 113 matrix-core compute only, 117 staging only by LDS-DMA, 110/111 streaming ceiling
+// of this traffic mix (plain / non-temporal).
 hipError_t launch_fc_probe(const FirJob& j, hipStream_t s);
 
 template <class TapT, class InT, int MODE>

@@ -679,6 +679,92 @@ __device__ __forceinline__ void poly_compute(const float4* __restrict__ lds, con
 }
 
 // ------------------------------------------------------------------------------------------------
+// Exact zero-padding semantics. The tiled cores round T up to whole tap chunks and multiply the
+// padding (taps read as +0 past T) like any other tap. For a finite sample x*0 is a signed zero and
+// adding it leaves the sum unchanged, but for x = +-Inf or NaN it is NaN, which the reference never
+// computes: its loop stops at tap T-1 (fir.cu:29-31, 58-60). A padding product can therefore only turn
+// an output into NaN. So every output that came out non-finite (a NaN or Inf output: a cheap test, and
+// rare) is recomputed from the staged tile in the SAME MAC order with the padding products skipped --
+// exactly the fast path's sum whenever no padding product was NaN, and the reference's set of products
+// otherwise. The result depends only on the output's own window, never on the tiling, so chunked and
+// monolithic calls stay bit-identical.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool finite_out(float a) { return __builtin_isfinite(a); }
+__device__ __forceinline__ bool finite_out(float2 a) { return __builtin_isfinite(a.x) && __builtin_isfinite(a.y); }
+
+struct NoPad {
+  __host__ __device__ static constexpr uint32_t padded(uint32_t g) { return g; }
+};
+
+// sample s of the tile (local index) from the LDS granule layout (padded as TileGeo when PADDED)
+template <class InT, class Geo, bool PADDED>
+__device__ __forceinline__ typename LdsSample<InT>::type tile_sample(const float4* __restrict__ lds, uint32_t s) {
+  using LdsT = typename LdsSample<InT>::type;
+  constexpr uint32_t G = SampleT<InT>::kPerGranule;
+  const uint32_t g = s / G;
+  const uint32_t slot = PADDED ? Geo::padded(g) : g;
+  return reinterpret_cast<const LdsT*>(lds)[slot * G + s % G];
+}
+
+// Polyphase order (poly_compute): chunk c, granule column h, row j, element e -- tap
+// i = (c*JC + j)*D + h*G + e of local output m = threadIdx.x * R + r.
+template <class TapT, class InT, int D, int R, int JC, int WG>
+__device__ __forceinline__ void poly_fixup(const float4* __restrict__ lds, const FirParams& p,
+                                        typename Product<TapT, InT>::type (&acc)[R]) {
+  using Geo = TileGeo<InT, D, R, WG>;
+  constexpr int G = Geo::G, CPR = D / G;
+  const TapT* __restrict__ taps = reinterpret_cast<const TapT*>(p.taps);
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    if (finite_out(acc[r])) continue;
+    const uint32_t s0 = (threadIdx.x * R + r) * D;
+    typename Product<TapT, InT>::type a;
+    set_zero(a);
+#pragma unroll 1
+    for (uint32_t c = 0; c < p.nch; ++c) {
+#pragma unroll 1
+      for (int h = 0; h < CPR; ++h) {
+#pragma unroll 1
+        for (int j = 0; j < JC; ++j) {
+          const uint32_t i0 = (c * JC + j) * D + h * G;
+#pragma unroll
+          for (int e = 0; e < G; ++e) {
+            if (i0 + e < p.T) mac(a, tile_sample<InT, Geo, true>(lds, s0 + i0 + e), taps[i0 + e]);
+          }
+        }
+      }
+    }
+    acc[r] = a;
+  }
+}
+
+// Ascending tap order (contiguous-window, runtime-decimation and matrix-core cores): local output m at
+// local sample m * D.
+template <class TapT, class InT, class Geo, bool PADDED, int R>
+__device__ __forceinline__ void ascending_fixup(const float4* __restrict__ lds, const FirParams& p, uint32_t D,
+                                             uint32_t m0, typename Product<TapT, InT>::type (&acc)[R]) {
+  const TapT* __restrict__ taps = reinterpret_cast<const TapT*>(p.taps);
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    if (finite_out(acc[r])) continue;
+    const uint32_t s0 = (m0 + r) * D;
+    typename Product<TapT, InT>::type a;
+    set_zero(a);
+#pragma unroll 1
+    for (uint32_t i = 0; i < p.T; ++i) mac(a, tile_sample<InT, Geo, PADDED>(lds, s0 + i), taps[i]);
+    acc[r] = a;
+  }
+}
+
+template <class OutT, int R>
+__device__ __forceinline__ bool all_finite(const OutT (&acc)[R]) {
+  bool ok = true;
+#pragma unroll
+  for (int r = 0; r < R; ++r) ok = ok && finite_out(acc[r]);
+  return ok;
+}
+
+// ------------------------------------------------------------------------------------------------
 // Kernel 1: polyphase-granule kernel, one tile per workgroup (D a multiple of the granule width G).
 // ABL (ablation, tuning probes only): 0 = full kernel, 1 = staging only, 2 = compute only.
 // NT: non-temporal (streaming) HBM loads for the staged input.
@@ -725,6 +811,9 @@ __global__ __launch_bounds__(WG) void k_fir_poly(FirParams p) {
     for (int r = 0; r < R; ++r) mac(acc[r], granule_sample<typename LdsSample<InT>::type>(v, r % G), 1.0f);
   } else {
     poly_compute<TapT, InT, D, R, JC, WG>(lds, p, acc);
+    if constexpr (ABL == 0) {
+      if (!all_finite(acc)) poly_fixup<TapT, InT, D, R, JC, WG>(lds, p, acc);
+    }
   }
 
   if constexpr (CST != 0 && MODE == kModeFir) {
@@ -812,6 +901,7 @@ __global__ __launch_bounds__(WG) void k_fir_multi(FirParams p, MultiParams mp) {
 #pragma unroll
     for (int r = 0; r < R; ++r) set_zero(acc[r]);
     poly_compute<TapT, InT, D, R, JC, WG>(lds, pc, acc);
+    if (!all_finite(acc)) poly_fixup<TapT, InT, D, R, JC, WG>(lds, pc, acc);
     tile_epilogue<MODE, OutT, R, WG>(pc, out0, acc, xs);
     __syncthreads();  // the next channel overwrites the tile
   }
@@ -865,6 +955,8 @@ __global__ __launch_bounds__(WG) void k_fir_contig(FirParams p) {
       }
     }
   }
+
+  if (!all_finite(acc)) ascending_fixup<TapT, InT, Geo, true, R>(lds, p, D, t * R, acc);
 
   float2* xs = reinterpret_cast<float2*>(lds + Geo::padded(NG - 1) + 1);
   tile_epilogue<MODE, OutT, R, WG>(p, out0, acc, xs);
@@ -921,6 +1013,7 @@ __global__ __launch_bounds__(WG) void k_fir_rt(FirParams p) {
     for (int i = 0; i < IC; ++i) mac(acc, xc[i], tv[i]);
   }
   OutT accs[1] = {acc};
+  if (!finite_out(acc)) ascending_fixup<TapT, InT, NoPad, false, 1>(lds, p, D, tid, accs);
   float2* ex = reinterpret_cast<float2*>(lds + NG);
   tile_epilogue<MODE, OutT, 1, WG>(p, out0, accs, ex);
 }
@@ -1044,6 +1137,9 @@ __global__ __launch_bounds__(WG) void k_fir_mfma_bc(FirParams p) {
   float2 acc[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) acc[r] = make_float2(cre[r], cim[r]);
+  if constexpr (ABL == 0) {
+    if (!all_finite(acc)) ascending_fixup<float, float2, Geo, true, R>(lds, p, D, tid * R, acc);
+  }
   tile_epilogue<kModeFir, float2, R, WG, NT>(p, out0, acc, nullptr);
 }
 

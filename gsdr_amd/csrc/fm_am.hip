@@ -100,8 +100,9 @@ static hipError_t chain_multi_entry(int mode, float fs, float tune, const float*
       e = mode == kModeFm ? launch_multi_chain<InT, kModeFm>(job, mp, stream)
                           : launch_multi_chain<InT, kModeAm>(job, mp, stream);
     }
-    if (e == hipErrorNotSupported) {  // one channel at a time through the single-channel path
-      (void)hipGetLastError();
+    // launch_multi_chain returns hipErrorNotSupported before launching anything (so there is no
+    // sticky launch error of ours to clear): one channel at a time through the single-channel path
+    if (e == hipErrorNotSupported) {
       e = hipSuccess;
       for (uint32_t c = 0; c < n && e == hipSuccess; ++c) {
         e = chain_entry(mode, fs, tune, chans[c0 + c], mode == kModeFm ? devs[c0 + c] : 1.0f, decimation,

@@ -466,10 +466,11 @@ GSDR_C_LINKAGE hipError_t gsdrQpsk256InitConstellation(uint32_t constellationTyp
     gsdr::build_cells(table, &cells);
     st = hipMemcpyToSymbolAsync(HIP_SYMBOL(gsdr::g_circ_cells), &cells, sizeof(cells), 0, hipMemcpyHostToDevice,
                                 cudaStream);
-    if (st != hipSuccess) return st;
   }
-  // the host table lives on this stack frame: wait for the copy before returning
-  return hipStreamSynchronize(cudaStream);
+  // the host table lives on this stack frame: wait for the copies before returning -- on every path
+  // once the first copy was issued, so a failed second copy cannot leave the first reading a dead frame
+  const hipError_t sync = hipStreamSynchronize(cudaStream);
+  return st != hipSuccess ? st : sync;
 }
 
 GSDR_C_LINKAGE hipError_t gsdrQpsk256Modulate(const uint8_t* inputBytes, hipFloatComplex* output, uint32_t numSymbols,

@@ -94,12 +94,14 @@ def fir(taps: torch.Tensor, x: torch.Tensor, decimation: int = 1, num_outputs: i
 
 def fir_variant(variant: int, taps: torch.Tensor, x: torch.Tensor, decimation: int = 4,
                 num_outputs: int | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
-    """gsdrFirFC with an explicit tile shape (tuning; see gsdr_ext.h)."""
+    """gsdrFirFC (complex64 input) or gsdrxFirFCInt8 (int8 I/Q input) with an explicit tile shape
+    (tuning; see gsdr_ext.h)."""
     name, n, out = _fir_prepare(taps, x, decimation, num_outputs, out)
-    if name != "gsdrFirFC":
-        raise TypeError("fir_variant is FC only")
-    check("gsdrxFirFCVariant", lib.gsdrxFirFCVariant(variant, decimation, _ptr(taps), taps.numel(), _ptr(x),
-                                                     _ptr(out), n, _dev(x), stream_of(x)))
+    if name not in ("gsdrFirFC", "gsdrxFirFCInt8"):
+        raise TypeError("fir_variant takes real taps on complex64 or int8 I/Q input")
+    entry = "gsdrxFirFCVariant" if name == "gsdrFirFC" else "gsdrxFirFCInt8Variant"
+    check(entry, getattr(lib, entry)(variant, decimation, _ptr(taps), taps.numel(), _ptr(x), _ptr(out), n, _dev(x),
+                                     stream_of(x)))
     return out
 
 

@@ -7,6 +7,7 @@
 #include <gsdr/am.h>
 #include <gsdr/arithmetic.h>
 #include <gsdr/conversion.h>
+#include <gsdr/cuda_util.h>
 #include <gsdr/fir.h>
 #include <gsdr/fm.h>
 #include <gsdr/gsdr_ext.h>

@@ -21,8 +21,13 @@
  * Sample formats: GSDRX_SAMPLES_CF32 (hipFloatComplex) or GSDRX_SAMPLES_CS8 (interleaved int8 I/Q,
  * the gsdrx*Int8 entry points of gsdr_ext.h).
  *
- * Threading: one object is one stream; calls on it must be ordered (same hipStream_t, or the caller
- * orders them). The taps buffer is the caller's and must stay valid while the object is used.
+ * Threading and streams: one object is one signal stream, and every gsdrxStreamProcess call on it must
+ * be given the SAME hipStream_t. The object keeps its history in two device buffers used alternately
+ * (each call reads the previous call's history buffer and writes the other one, with no event or
+ * synchronisation between calls), so the calls are ordered only by the HIP stream they share: feeding
+ * one object from two HIP streams lets call k+1 read the history before call k has written it. To move
+ * an object to another HIP stream, synchronise the old one first. Do not call one object from two host
+ * threads concurrently. The taps buffer is the caller's and must stay valid while the object is used.
  */
 #ifndef GSDR_STREAM_H_
 #define GSDR_STREAM_H_

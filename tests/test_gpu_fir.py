@@ -111,17 +111,62 @@ def test_fir_restores_current_device(cuda):
     assert torch.cuda.current_device() == 0
 
 
-@pytest.mark.parametrize("variant", [0, 1, 3, 4, 5, 7, 8, 9, 10, 11, 13, 14, 24, 28])
-def test_fir_fc_d4_variants(cuda, variant):
-    """Every tile shape of the headline kernel (gsdrxFirFCVariant) meets the same bar."""
+# Tile shapes of gsdrxFirFCVariant (fir_dispatch.hpp launch_d4_complex). The per-output MAC order of
+# the polyphase kernels depends only on (D, JC), so the JC = 16 shapes must equal variant 0 bit for
+# bit; the generic kernel (7) and the matrix-core core (13) sum in ascending tap order, like the oracle.
+VARIANTS_JC16 = [0, 1, 3, 8, 9, 10, 11, 14, 24, 28]
+VARIANTS_OTHER_ORDER = [4, 5]  # JC = 32 / JC = 8: own MAC order, normwise bar
+VARIANTS_ASCENDING = [7, 13]
+INT8_VARIANTS = [0, 1, 3, 4, 5, 7, 24, 28]  # launch_d4_int8
+
+
+@pytest.mark.parametrize("T", [127, 63, 200])
+@pytest.mark.parametrize("variant", VARIANTS_JC16 + VARIANTS_OTHER_ORDER + VARIANTS_ASCENDING)
+def test_fir_fc_d4_variants(cuda, variant, T):
+    """Every exported tile shape of the headline kernel (gsdrxFirFCVariant) against the oracle."""
     from gsdr_amd import ops
 
-    N, D, T = 50000 + 3, 4, 127
-    taps, x = make("FC", T, (N - 1) * D + T, 99)
-    y = ops.fir_variant(13, dev(taps, cuda), dev(x, cuda), D, N)
-    torch.cuda.synchronize()
+    if variant == 13 and T > 132:
+        pytest.skip("variant 13 holds at most 132 taps in registers (returns hipErrorInvalidValue)")
+    N, D = 50000 + 3, 4
+    taps, x = make("FC", T, (N - 1) * D + T, 99 + T)
+    td, xd = dev(taps, cuda), dev(x, cuda)
+    y = ops.fir_variant(variant, td, xd, D, N).cpu().numpy()
     ref = o.fir(taps, x, D, N)
-    assert np.array_equal(y.cpu().numpy().view(np.uint64), ref.view(np.uint64))
+    if variant in VARIANTS_ASCENDING:
+        assert np.array_equal(y.view(np.uint64), ref.view(np.uint64))
+    else:
+        assert normwise_err(y, ref, bound(taps, x, D, N)) <= FLOAT_TOL
+    if variant in VARIANTS_JC16:
+        y0 = ops.fir_variant(0, td, xd, D, N).cpu().numpy()
+        assert np.array_equal(y.view(np.uint64), y0.view(np.uint64))
+
+
+def test_fir_fc_d4_variant_13_rejects_long_filters(cuda):
+    from gsdr_amd import GsdrError, ops
+
+    taps, x = make("FC", 133, 3 * 4 + 133, 5)
+    with pytest.raises(GsdrError):
+        ops.fir_variant(13, dev(taps, cuda), dev(x, cuda), 4, 4)
+
+
+@pytest.mark.parametrize("variant", INT8_VARIANTS)
+def test_fir_int8_d4_variants(cuda, variant):
+    """gsdrxFirFCInt8Variant: each shape is bit-identical to gsdrxFirFCVariant of the same shape on the
+    converted samples (the conversion exists only in LDS), and meets the bar against the oracle."""
+    from gsdr_amd import ops
+
+    N, D, T = 20000 + 5, 4, 127
+    taps = make("FC", T, 1, 11)[0]
+    rng = np.random.default_rng(variant)
+    x8 = torch.from_numpy(rng.integers(-128, 128, 2 * ((N - 1) * D + T), dtype=np.int8)).to(cuda)
+    td = dev(taps, cuda)
+    y8 = ops.fir_variant(variant, td, x8, D, N)
+    xf = ops.int8_to_norm_float(x8).view(torch.complex64)
+    yf = ops.fir_variant(variant, td, xf, D, N)
+    assert torch.equal(y8.view(torch.float32), yf.view(torch.float32))
+    xh = xf.cpu().numpy()
+    assert normwise_err(y8.cpu().numpy(), o.fir(taps, xh, D, N), bound(taps, xh, D, N)) <= FLOAT_TOL
 
 
 @pytest.mark.parametrize("T", [1, 2, 3, 4, 5, 8, 63, 116, 117, 127, 128, 132])

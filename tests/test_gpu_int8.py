@@ -141,3 +141,27 @@ def test_fir_int8_shifted_staging_bit_identical(cuda, D, offset_bytes):
     y0 = host(ops.fir(taps, aligned, D, n))
     y1 = host(ops.fir(taps, buf[offset_bytes:offset_bytes + 2 * L], D, n))
     assert y1.tobytes() == y0.tobytes()
+
+
+@pytest.mark.parametrize("mode", ["fm_demod", "am_demod"])
+@pytest.mark.parametrize("offset_bytes", [2, 4, 6])
+@pytest.mark.parametrize("D", [1, 2, 3, 4, 5, 8])
+def test_chain_int8_misaligned_bit_identical(cuda, mode, D, offset_bytes):
+    """FM / AM chains from int8 I/Q at 2-, 4- and 6-byte offsets (odd-sample offsets take the shifted
+    staging, whose first pair starts one sample early and is mixed with the odd-index NCO phasor; FM at
+    odd D also has the two-output tile overlap): bit-identical to the same samples at an aligned
+    address, with the same firstSampleIndex."""
+    from gsdr_amd import ops
+
+    T, n, n0 = 127, 30000, 12345
+    L = n * D + T
+    raw = iq8(L + 8, seed=100 + D)
+    taps = dev(taps_for(T), cuda)
+    buf = dev(raw, cuda)
+    aligned = torch.empty(2 * L + 16, dtype=torch.int8, device=buf.device)[:2 * L]
+    aligned.copy_(buf[offset_bytes:offset_bytes + 2 * L])
+    args = (1.0e6, 0.0, 1.0e5, 2.0e4) if mode == "fm_demod" else (1.0e6, 0.0, 1.0e5)
+    fn = getattr(ops, mode)
+    y0 = host(fn(aligned, taps, *args, D, n0, n))
+    y1 = host(fn(buf[offset_bytes:offset_bytes + 2 * L], taps, *args, D, n0, n))
+    assert y1.tobytes() == y0.tobytes()

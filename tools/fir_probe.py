@@ -7,6 +7,9 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# ablation variants (>= 100) exist only in the tuning-probe build (`make probes`)
+os.environ.setdefault("GSDR_LIB", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "build",
+                                               "probes", "libgsdr_probes.so"))
 
 import torch  # noqa: E402
 

@@ -22,6 +22,7 @@ _u32 = ctypes.c_uint32
 _i32 = ctypes.c_int32
 _int = ctypes.c_int
 _f = ctypes.c_float
+_u64 = ctypes.c_uint64
 _err = ctypes.c_int  # hipError_t
 
 
@@ -74,6 +75,7 @@ SIGNATURES = {
     "gsdrQpskDemodulateTemplated": (_err, [_p, _p, _u32, _int, _i32, _p]),
     # qpsk256.h
     "gsdrQpsk256Modulate": (_err, [_p, _p, _u32, _f, _u32, _i32, _p]),
+    "gsdrxQpsk256ModulateAwgn": (_err, [_p, _p, _u32, _u32, _f, _u64, _u64, _i32, _p]),
     "gsdrQpsk256Demodulate": (_err, [_p, _p, _u32, _u32, _i32, _p]),
     "gsdrQpsk256Modulate4x": (_err, [_p, _p, _p, _p, _p, _p, _p, _p, _u32, _f, _u32, _i32, _p]),
     "gsdrQpsk256Demodulate4x": (_err, [_p, _p, _p, _p, _p, _p, _p, _p, _u32, _u32, _i32, _p]),

@@ -67,6 +67,31 @@ hipError_t launch_fc_probe(const FirJob& j, hipStream_t s) {
       return launch_mfma_bc<256, 9, 2>(j, s);
     case 117:  // staging only by LDS-DMA, non-temporal
       return launch_poly<float, float2, 4, 4, 16, 256, kModeFir, 1, true, false, 0, true>(j, s);
+    // FM chain (config 3 shape) split: 120 full FM kernel, 121 no NCO mix, 122 no discriminator (plain
+    // float store), 123 neither, 124 staging + NCO + discriminator without the FIR, 125 staging only,
+    // 126 NCO mix without its per-granule transcendental pair
+    case 120:
+    case 121:
+    case 122:
+    case 123:
+    case 124:
+    case 125:
+    case 126: {
+      FirJob c = j;
+      c.mode = kModeFm;
+      c.N = j.N - 1;  // an FM output needs one more FIR output than the input holds for N FIR outputs
+      c.nco_inc = 429496730u;  // 0.1 fs
+      c.fm_gain = 7.957747f;   // fs / (2 pi 0.02 fs)
+      switch (j.variant) {
+        case 120: return launch_poly<float, float2, 4, 4, 16, 256, kModeFm, 0, true>(c, s);
+        case 121: return launch_poly<float, float2, 4, 4, 16, 256, kModeFm, 8, true>(c, s);
+        case 122: return launch_poly<float, float2, 4, 4, 16, 256, kModeFm, 16, true>(c, s);
+        case 123: return launch_poly<float, float2, 4, 4, 16, 256, kModeFm, 24, true>(c, s);
+        case 124: return launch_poly<float, float2, 4, 4, 16, 256, kModeFm, 1, true>(c, s);
+        case 126: return launch_poly<float, float2, 4, 4, 16, 256, kModeFm, 32, true>(c, s);
+        default: return launch_poly<float, float2, 4, 4, 16, 256, kModeFm, 25, true>(c, s);
+      }
+    }
     case 110:
     case 111:
       return launch_stream_probe(j, s, j.variant == 111);

@@ -285,13 +285,16 @@ __device__ __forceinline__ float4 load_granule(const InT* __restrict__ in, uint6
 // its first sample; `odd` = n & 1 (wave-uniform in the tiled kernels: they stage granules at even
 // offsets from the tile start). The phasor is a pure function of the absolute index: even n from
 // nco_direct, odd n = phasor(n - 1) * w, w = nco_direct(inc).
-template <class InT, int MODE>
+template <class InT, int MODE, bool NODIRECT = false>
 __device__ __forceinline__ float4 stage_transform_ph(float4 v, uint32_t ph, bool odd, uint32_t inc) {
   if constexpr (MODE != kModeFir) {
     static_assert(SampleT<InT>::kPerGranule == 2, "NCO modes take complex input");
     const float2 w = nco_direct(inc);
     float2 ea, eb;
-    if (odd) {
+    if constexpr (NODIRECT) {  // tuning probe only: the per-granule transcendental pair left out
+      ea = make_float2(w.y, w.x);
+      eb = cmul(ea, w);
+    } else if (odd) {
       ea = cmul(nco_direct(ph - inc), w);
       eb = nco_direct(ph + inc);
     } else {
@@ -377,7 +380,8 @@ __device__ __forceinline__ bool stage_body_dma(float4* __restrict__ lds, const I
 // split over two LDS granules (second half of slot g - 1, first half of slot g); the halo re-writes the
 // body's last slot whole. The NCO phasor is a function of the absolute index, so the odd-start pairs
 // mix exactly as the even-start ones would.
-template <class InT, class Geo, int WG, bool VEC, int MODE, bool NT = false, bool DMA = false, bool SH = false>
+template <class InT, class Geo, int WG, bool VEC, int MODE, bool NT = false, bool DMA = false, bool SH = false,
+          bool NODIRECT = false>
 __device__ __forceinline__ void stage_tile(float4* __restrict__ lds, const InT* __restrict__ in, uint64_t S0,
                                            uint32_t NG, const FirParams& p) {
   constexpr int G = Geo::G;
@@ -479,7 +483,8 @@ __device__ __forceinline__ void stage_tile(float4* __restrict__ lds, const InT* 
 #pragma unroll
     for (int k = 0; k < SB; ++k) {
       const uint32_t g = (b0 + k) * WG + tid;
-      lds[Geo::padded(g)] = stage_transform_ph<InT, MODE>(v[k], pw.ph0 + (uint32_t)(b0 + k) * pw.step, pw.odd, pw.inc);
+      lds[Geo::padded(g)] =
+          stage_transform_ph<InT, MODE, NODIRECT>(v[k], pw.ph0 + (uint32_t)(b0 + k) * pw.step, pw.odd, pw.inc);
     }
   }
   for (uint32_t g = BPT * WG + tid; g < NG; g += WG) {
@@ -756,17 +761,38 @@ __device__ __forceinline__ void ascending_fixup(const float4* __restrict__ lds, 
   }
 }
 
-template <class OutT, int R>
-__device__ __forceinline__ bool all_finite(const OutT (&acc)[R]) {
-  bool ok = true;
+// Wave-cheap screen for the fix-up: the sum of a thread's outputs is finite when they all are (a NaN or
+// Inf term makes it NaN or Inf). A finite set whose sum overflows only sends the thread through the
+// per-output test in the fix-up, which then changes nothing. Packed adds: 5 VALU operations for R = 4
+// complex outputs instead of one class test per component.
+typedef float gsdr_f32x2 __attribute__((ext_vector_type(2)));
+template <int R>
+__device__ __forceinline__ bool all_finite(const float2 (&acc)[R]) {
+  gsdr_f32x2 s = {acc[0].x, acc[0].y};
 #pragma unroll
-  for (int r = 0; r < R; ++r) ok = ok && finite_out(acc[r]);
-  return ok;
+  for (int r = 1; r < R; ++r) s += gsdr_f32x2{acc[r].x, acc[r].y};
+  return __builtin_isfinite(s.x + s.y);
+}
+template <int R>
+__device__ __forceinline__ bool all_finite(const float (&acc)[R]) {
+  if constexpr (R % 2 == 0) {
+    gsdr_f32x2 s = {acc[0], acc[1]};
+#pragma unroll
+    for (int r = 2; r < R; r += 2) s += gsdr_f32x2{acc[r], acc[r + 1]};
+    return __builtin_isfinite(s.x + s.y);
+  } else {
+    float s = acc[0];
+#pragma unroll
+    for (int r = 1; r < R; ++r) s += acc[r];
+    return __builtin_isfinite(s);
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
 // Kernel 1: polyphase-granule kernel, one tile per workgroup (D a multiple of the granule width G).
-// ABL (ablation, tuning probes only): 0 = full kernel, 1 = staging only, 2 = compute only.
+// ABL (ablation, tuning probes only): low bits 0 = full kernel, 1 = staging only, 2 = compute only;
+// chain-mode flags 8 = staging without the NCO mix, 16 = plain float store instead of the FM
+// discriminator, 32 = NCO mix without the per-granule transcendental pair.
 // NT: non-temporal (streaming) HBM loads for the staged input.
 // ------------------------------------------------------------------------------------------------
 // Tile of workgroup b. XCD-aware (XM): workgroups are dispatched round-robin over the 8 XCDs, so
@@ -799,13 +825,14 @@ __global__ __launch_bounds__(WG) void k_fir_poly(FirParams p) {
   const uint32_t span = p.nch * JC * D;
   const uint32_t NG = ((Geo::KT - 1) * D + span + G - 1) / G;
   // LDS: [tile granules | FM exchange (WG float2)]
-  if constexpr (ABL != 2) stage_tile<InT, Geo, WG, VEC, MODE, NT, DMA, SH>(lds, in, S0, NG, p);
+  constexpr int SMODE = (ABL & 8) ? (int)kModeFir : MODE;
+  if constexpr ((ABL & 7) != 2) stage_tile<InT, Geo, WG, VEC, SMODE, NT, DMA, SH, (ABL & 32) != 0>(lds, in, S0, NG, p);
   __syncthreads();
 
   OutT acc[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) set_zero(acc[r]);
-  if constexpr (ABL == 1) {
+  if constexpr ((ABL & 7) == 1) {
     const float4 v = lds[Geo::padded(threadIdx.x * Geo::SG)];
 #pragma unroll
     for (int r = 0; r < R; ++r) mac(acc[r], granule_sample<typename LdsSample<InT>::type>(v, r % G), 1.0f);
@@ -818,6 +845,15 @@ __global__ __launch_bounds__(WG) void k_fir_poly(FirParams p) {
 
   if constexpr (CST != 0 && MODE == kModeFir) {
     if (store_tile_lds<CST, OutT, R, WG>(lds, p, out0, acc)) return;
+  }
+  if constexpr ((ABL & 16) != 0 && MODE == kModeFm) {
+    float* out = reinterpret_cast<float*>(p.out);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint32_t ml = threadIdx.x * R + r;
+      if (ml < p.tile_stride && out0 + ml < p.N) out[out0 + ml] = acc[r].x + acc[r].y;
+    }
+    return;
   }
   float2* xs = reinterpret_cast<float2*>(lds + Geo::padded(NG - 1) + 1);
   tile_epilogue<MODE, OutT, R, WG, NT>(p, out0, acc, xs);

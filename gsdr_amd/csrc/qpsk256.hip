@@ -7,20 +7,26 @@
 // copies the 2 KiB table it needs into LDS, so lookups are LDS reads rather than divergent
 // constant-cache accesses.
 //
-// Demodulation decision (bit-exact contract shared with the CPU oracle): the first index attaining
-// the minimum of d_i = fl(fl(dx*dx) + fl(dy*dy)) over all 256 points, strict '<', d initialised to
-// +inf (so a NaN/inf symbol maps to 0), as the reference's exhaustive argmin (qpsk256.cu:171-181) with
-// the squared distance in place of cuCabsf. For the rectangular grid a received point inside
+// Demodulation decision: the reference's own rule (qpsk256.cu:171-181), bit for bit -- the first index
+// attaining the minimum of cuCabsf(received - point) over all 256 points, strict '<', initialised to
+// +inf (so a NaN/inf symbol maps to 0). cuCabsf is CUDA cuComplex.h's scaled hypot (ref_cabsf below),
+// with `1 + t*t` contracted to one fma as nvcc does by default. The fast paths rank candidates by the
+// cheaper squared distance s_i = fl(fl(dx*dx) + fl(dy*dy)) of the same rounded differences: when the
+// smallest s beats every other candidate by a relative margin of 2^-18, which is far wider than the
+// combined rounding of s (2^-23) and of cuCabsf (about 4 ulp), the cuCabsf order agrees and that
+// candidate is the reference's answer. Otherwise (a near-tie) the candidates are re-ranked with
+// cuCabsf itself in ascending index order. For the rectangular grid a received point inside
 // |re|,|im| <= 4|a| can only be won by one of the 3 x 3 grid points around its per-axis nearest level
-// (every other point is farther by >= 0.035 a^2, far beyond float rounding), so those 9 candidates are
-// evaluated in ascending index order with the identical expression; anything else takes the
-// exhaustive path. Circular tables always take the exhaustive path.
+// (every other point is farther by >= 0.035 a^2); circular tables use per-cell candidate lists;
+// anything else takes the exhaustive cuCabsf search.
 #include <hip/hip_runtime.h>
 #include <math.h>
 
 #include <algorithm>
 #include <cmath>
 
+#include "awgn.hpp"
+#include "gsdr/gsdr_ext.h"
 #include "gsdr/qpsk256.h"
 #include "launch.hpp"
 
@@ -37,7 +43,8 @@ __constant__ float2 c_qpsk256_tables[2][256];
 // A point is listed for a cell when its distance to the cell is at most the smallest worst-case
 // distance of any table point over the cell (plus a margin for float rounding), so every point that
 // can win the argmin anywhere in the cell -- ties included -- is on the list, and the argmin over the
-// list in index order with the same sqdist() is the exhaustive one. R == 0 disables the lookup.
+// list in index order is the exhaustive one -- for the squared distance and, with the near-tie
+// re-ranking of the demodulation kernel, for the reference's cuCabsf rule. R == 0 disables the lookup.
 constexpr int kCellGrid = 96;
 constexpr int kMaxCellEntries = 19456;  // 18,764 used by the circular table (any amplitude); LDS < 40 KB
 constexpr double kCellSpan = 1.3;  // grid half-width R = 1.3 * max |c|: noisy symbols stay on the grid
@@ -60,11 +67,31 @@ __device__ __forceinline__ float sqdist(float2 r, float2 c) {
   return __fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy));
 }
 
+// cuCabsf (CUDA cuComplex.h, called at qpsk256.cu:173, 182): v = max(|a|, |b|), w = min, t = w / v,
+// |z| = v * sqrt(fma(t, t, 1)), v + w when v == 0 or either exceeds FLT_MAX. IEEE division and square
+// root, as nvcc's defaults (-prec-div, -prec-sqrt) give.
+__device__ __forceinline__ float ref_cabsf(float re, float im) {
+  const float a = fabsf(re), b = fabsf(im);
+  const float v = a > b ? a : b;
+  const float w = a > b ? b : a;
+  float t = __fdiv_rn(w, v);
+  t = fmaf(t, t, 1.0f);
+  t = __fmul_rn(v, __fsqrt_rn(t));
+  if (v == 0.0f || v > 3.402823466e38f || w > 3.402823466e38f) t = __fadd_rn(v, w);
+  return t;
+}
+
+// the reference's distance of received point r to table point c (cuCsubf, then cuCabsf)
+__device__ __forceinline__ float ref_dist(float2 r, float2 c) { return ref_cabsf(__fsub_rn(r.x, c.x), __fsub_rn(r.y, c.y)); }
+
+// fast-path acceptance: every other candidate's squared distance exceeds s_min by 2^-18 relative
+__device__ __forceinline__ float tie_threshold(float smin) { return fmaf(smin, 0x1p-18f, smin); }
+
 __device__ __noinline__ uint32_t demod_exhaustive(const float2* __restrict__ tab, float2 r) {
   float best = INFINITY;
   uint32_t idx = 0;
   for (uint32_t i = 0; i < 256; ++i) {
-    const float d = sqdist(r, tab[i]);
+    const float d = ref_dist(r, tab[i]);
     if (d < best) {
       best = d;
       idx = i;
@@ -88,23 +115,24 @@ __device__ __forceinline__ int nearest_level(float v, float scale) {
 //
 // The 3 x 3 neighbourhood of the per-axis nearest levels contains the exhaustive argmin for
 // |re|,|im| <= 4|a|. Rounded addition is monotone in each operand, so with a = first argmin of ex and
-// b = first argmin of ey the minimum is dmin = fl(ex[a] + ey[b]), and (a, b) is the ONLY candidate
-// reaching it when the second-smallest ex plus ey[b], and ex[a] plus the second-smallest ey, both
-// exceed dmin (any other candidate is >= one of those two sums). Then it is the exhaustive answer;
-// otherwise (a rounding tie near a decision boundary) the 9 candidates are scanned in index order
-// with strict '<', as the exhaustive search does. Returns 256 when the symbol needs the exhaustive
-// search (outside |re|,|im| <= 4|a|, or NaN).
+// b = first argmin of ey the minimum is dmin = fl(ex[a] + ey[b]), and every other candidate is >= the
+// second-smallest ex plus ey[b], or >= ex[a] plus the second-smallest ey. When both of those exceed
+// dmin by the 2^-18 margin, (a, b) is the reference's answer; otherwise (a near-tie at a decision
+// boundary) the 9 candidates are ranked by cuCabsf in ascending index order with strict '<', as the
+// reference's exhaustive loop does (no point outside the 3 x 3 can be that close). Returns 256 when the
+// symbol needs the exhaustive search (outside |re|,|im| <= 4|a|, or NaN).
 __device__ __forceinline__ uint32_t demod_rect_fast(const float* __restrict__ lxp, const float* __restrict__ lyp, float2 r,
                                                     float lim, float scale) {
   if (!(fabsf(r.x) <= lim && fabsf(r.y) <= lim)) return 256u;
   const int i0 = nearest_level(r.x, scale);
   const int q0 = nearest_level(r.y, scale);
-  float ex[3], ey[3];
+  float dx[3], dy[3], ex[3], ey[3];
 #pragma unroll
   for (int d = 0; d < 3; ++d) {
-    const float dx = __fsub_rn(r.x, lxp[i0 + d]), dy = __fsub_rn(r.y, lyp[q0 + d]);
-    ex[d] = __fmul_rn(dx, dx);
-    ey[d] = __fmul_rn(dy, dy);
+    dx[d] = __fsub_rn(r.x, lxp[i0 + d]);
+    dy[d] = __fsub_rn(r.y, lyp[q0 + d]);
+    ex[d] = __fmul_rn(dx[d], dx[d]);
+    ey[d] = __fmul_rn(dy[d], dy[d]);
   }
   const float exm = fminf(fminf(ex[0], ex[1]), ex[2]);
   const float eym = fminf(fminf(ey[0], ey[1]), ey[2]);
@@ -112,15 +140,16 @@ __device__ __forceinline__ uint32_t demod_rect_fast(const float* __restrict__ lx
   const float ey2 = __builtin_amdgcn_fmed3f(ey[0], ey[1], ey[2]);
   const int a = ex[0] == exm ? 0 : (ex[1] == exm ? 1 : 2);
   const int b = ey[0] == eym ? 0 : (ey[1] == eym ? 1 : 2);
-  const float dmin = __fadd_rn(exm, eym);
-  if (__fadd_rn(ex2, eym) > dmin && __fadd_rn(exm, ey2) > dmin) return (uint32_t)((i0 - 1 + a) * 16 + (q0 - 1 + b));
+  const float thr = tie_threshold(__fadd_rn(exm, eym));
+  if (__fadd_rn(ex2, eym) > thr && __fadd_rn(exm, ey2) > thr) return (uint32_t)((i0 - 1 + a) * 16 + (q0 - 1 + b));
   float best = INFINITY;
   uint32_t idx = 0;
 #pragma unroll
   for (int di = 0; di < 3; ++di) {
 #pragma unroll
     for (int dq = 0; dq < 3; ++dq) {
-      const float d = __fadd_rn(ex[di], ey[dq]);
+      // out-of-grid neighbours (padded +inf levels) give an infinite difference and never win
+      const float d = ref_cabsf(dx[di], dy[dq]);
       if (d < best) {
         best = d;
         idx = (uint32_t)((i0 - 1 + di) * 16 + (q0 - 1 + dq));
@@ -175,6 +204,52 @@ __global__ __launch_bounds__(kCBlock) void k_c256_mod(C256Streams st, uint32_t n
   } else {
     for (int k = 0; k < kCSym; ++k) {
       if (s0 + k < n) out[s0 + k] = tab[in[s0 + k]];
+    }
+  }
+}
+
+// Modulate + counter-based AWGN (gsdrxQpsk256ModulateAwgn; awgn.hpp). Lane t of slot q handles the
+// local symbol pair q * kCBlock + t of the block (coalesced byte-pair loads and 16-byte stores, as
+// k_c256_mod). With an even first absolute index a local pair is one Philox pair (one call for two
+// symbols); with an odd one its symbols straddle two Philox pairs (two calls).
+__global__ __launch_bounds__(kCBlock) void k_c256_mod_awgn(const uint8_t* __restrict__ in, float2* __restrict__ out,
+                                                            uint32_t n, uint32_t type, float sigma, uint64_t seed,
+                                                            uint64_t first) {
+  __shared__ float2 tab[256];
+  load_table(tab, type);
+  const bool odd0 = (first & 1u) != 0;
+  const uint64_t base = (uint64_t)blockIdx.x * kCBlock * kCSym;
+#pragma unroll 2
+  for (int q = 0; q < kCSym / 2; ++q) {
+    const uint64_t s = base + 2u * ((uint64_t)q * kCBlock + threadIdx.x);  // local symbol of the pair
+    if (s >= n) break;
+    const bool two = s + 1 < n;
+    const uint64_t a = first + s;  // absolute index of the first symbol
+    uint32_t w[4];
+    awgn_pair_words(seed, a >> 1, w);
+    float2 g0, g1;
+    if (!odd0) {
+      g0 = awgn_box_muller(w[0], w[1]);
+      g1 = awgn_box_muller(w[2], w[3]);
+    } else {
+      g0 = awgn_box_muller(w[2], w[3]);
+      uint32_t w2[4];
+      awgn_pair_words(seed, (a + 1) >> 1, w2);
+      g1 = awgn_box_muller(w2[0], w2[1]);
+    }
+    const float2 p0 = tab[in[s]];
+    const float2 y0 = make_float2(p0.x + sigma * g0.x, p0.y + sigma * g0.y);
+    if (two) {
+      const float2 p1 = tab[in[s + 1]];
+      const float2 y1 = make_float2(p1.x + sigma * g1.x, p1.y + sigma * g1.y);
+      if ((reinterpret_cast<uintptr_t>(out + s) & 15u) == 0) {
+        *reinterpret_cast<float4*>(out + s) = make_float4(y0.x, y0.y, y1.x, y1.y);
+      } else {
+        out[s] = y0;
+        out[s + 1] = y1;
+      }
+    } else {
+      out[s] = y0;
     }
   }
 }
@@ -244,10 +319,10 @@ __global__ __launch_bounds__(kCBlock) void k_c256_demod(C256Streams st, uint32_t
       if (cR > 0.0f && fx >= 0.0f && fy >= 0.0f && fx < (float)kCellGrid && fy < (float)kCellGrid) {
         const int c = (int)fy * kCellGrid + (int)fx;
         const uint32_t b = cstart[c], e = cstart[c + 1];
-        float best = INFINITY;
+        float best = INFINITY, second = INFINITY;
         uint32_t idx = 0;
         // four candidates per step with independent LDS loads; slots past the list end repeat its
-        // last entry, which cannot win again under strict '<'
+        // last entry (a duplicate of an entry already ranked: skipped for the runner-up)
         for (uint32_t m = b; m < e; m += 4) {
           uint32_t k[4];
           float2 pt[4];
@@ -257,11 +332,27 @@ __global__ __launch_bounds__(kCBlock) void k_c256_demod(C256Streams st, uint32_t
           for (int j = 0; j < 4; ++j) pt[j] = tab[k[j]];
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const float d = sqdist(r, pt[j]);
-            if (d < best) {  // ascending list: first index wins ties, as the exhaustive search
+            const float d = (j == 0 || m + j < e) ? sqdist(r, pt[j]) : INFINITY;
+            if (d < best) {
+              second = best;
               best = d;
               idx = k[j];
+            } else if (d < second) {
+              second = d;
             }
+          }
+        }
+        if (second > tie_threshold(best)) return idx;
+        // near-tie: the list (ascending indices, every point that can win in the cell) ranked by
+        // cuCabsf with strict '<', as the reference's loop
+        best = INFINITY;
+        idx = 0;
+        for (uint32_t m = b; m < e; ++m) {
+          const uint32_t k = cidx[m];
+          const float d = ref_dist(r, tab[k]);
+          if (d < best) {
+            best = d;
+            idx = k;
           }
         }
         return idx;
@@ -481,6 +572,23 @@ GSDR_C_LINKAGE hipError_t gsdrQpsk256Modulate(const uint8_t* inputBytes, hipFloa
   st.in[0] = inputBytes;
   st.out[0] = output;
   return gsdr::c256_launch(true, st, 1, numSymbols, constellationType, cudaDevice, cudaStream);
+}
+
+GSDR_C_LINKAGE hipError_t gsdrxQpsk256ModulateAwgn(const uint8_t* inputBytes, hipFloatComplex* output,
+                                                    uint32_t numSymbols, uint32_t constellationType, float sigma,
+                                                    uint64_t seed, uint64_t firstSymbolIndex, int32_t cudaDevice,
+                                                    hipStream_t cudaStream) GSDR_NO_EXCEPT {
+  if (numSymbols == 0) return hipSuccess;
+  if (inputBytes == nullptr || output == nullptr || !(sigma >= 0.0f) || !(sigma < INFINITY)) {
+    return hipErrorInvalidValue;
+  }
+  gsdr::DeviceScope scope(cudaDevice);
+  if (scope.status() != hipSuccess) return scope.status();
+  const uint32_t blocks =
+      (uint32_t)gsdr::ceil_div<uint64_t>(gsdr::ceil_div<uint64_t>(numSymbols, gsdr::kCSym), gsdr::kCBlock);
+  gsdr::k_c256_mod_awgn<<<dim3(blocks), dim3(gsdr::kCBlock), 0, cudaStream>>>(
+      inputBytes, reinterpret_cast<float2*>(output), numSymbols, constellationType, sigma, seed, firstSymbolIndex);
+  return gsdr::launch_status();
 }
 
 GSDR_C_LINKAGE hipError_t gsdrQpsk256Demodulate(const hipFloatComplex* input, uint8_t* outputBytes,

@@ -15,7 +15,7 @@ __all__ = [
     "fir", "fir_variant", "fm_demod", "am_demod", "quad_fm_demod", "quad_am_demod", "magnitude",
     "qpsk_modulate", "qpsk_demodulate", "qpsk_modulate_4x", "qpsk_demodulate_4x",
     "qpsk_modulate_templated", "qpsk_demodulate_templated",
-    "qpsk256_init", "qpsk256_modulate", "qpsk256_demodulate", "qpsk256_modulate_4x", "qpsk256_demodulate_4x",
+    "qpsk256_init", "qpsk256_modulate", "qpsk256_modulate_awgn", "qpsk256_demodulate", "qpsk256_modulate_4x", "qpsk256_demodulate_4x",
     "nco_phase_increment", "stream_of",
     "fm_demod_multi", "am_demod_multi", "iir", "add_const", "multiply", "add_to_magnitude", "abs_", "cosine", "int8_to_norm_float",
 ]
@@ -377,6 +377,18 @@ def qpsk256_modulate(symbols, constellation_type, amplitude=1.0, out=None):
     _require(out, torch.complex64, "output", n)
     check("gsdrQpsk256Modulate", lib.gsdrQpsk256Modulate(_ptr(symbols), _ptr(out), n, amplitude, constellation_type,
                                                          _dev(symbols), stream_of(symbols)))
+    return out
+
+
+def qpsk256_modulate_awgn(symbols, constellation_type, sigma, seed, first_symbol_index=0, out=None):
+    """gsdrxQpsk256ModulateAwgn: table[s] + sigma * counter-based Gaussian noise of (seed, absolute index)."""
+    _require(symbols, torch.uint8, "inputBytes")
+    n = symbols.numel()
+    out = torch.empty(n, dtype=torch.complex64, device=symbols.device) if out is None else out
+    _require(out, torch.complex64, "output", n)
+    check("gsdrxQpsk256ModulateAwgn", lib.gsdrxQpsk256ModulateAwgn(_ptr(symbols), _ptr(out), n, constellation_type,
+                                                                   sigma, seed, first_symbol_index, _dev(symbols),
+                                                                   stream_of(symbols)))
     return out
 
 

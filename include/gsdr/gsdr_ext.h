@@ -154,4 +154,27 @@ GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxAmDemodMulti(
     int32_t cudaDevice,
     hipStream_t cudaStream) GSDR_NO_EXCEPT;
 
+/*
+ * Config 5's channel model (BASELINE configs[4]: QPSK256 modulate -> AWGN -> demod): the output of
+ * gsdrQpsk256Modulate (the table set by gsdrQpsk256InitConstellation for constellationType) plus
+ * additive white Gaussian noise of standard deviation `sigma` per axis, in one pass:
+ *     output[k] = table[inputBytes[k]] + (sigma * g0, sigma * g1),  each component rounded once,
+ * where (g0, g1) are the standard normals of absolute symbol index firstSymbolIndex + k: Box-Muller
+ * over Philox4x32-10 keyed by `seed` (the exact construction is in gsdr_amd/csrc/awgn.hpp and its host
+ * restatement in oracle/gsdr_oracle.h), built from correctly rounded IEEE operations only. The noise
+ * is therefore a pure function of (seed, absolute index): a host can regenerate the noisy buffer bit
+ * for bit, and splitting a buffer over several calls (advancing firstSymbolIndex) yields the same
+ * samples. Returns hipErrorInvalidValue for null pointers or a negative / non-finite sigma.
+ */
+GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxQpsk256ModulateAwgn(
+    const uint8_t* inputBytes,
+    hipFloatComplex* output,
+    uint32_t numSymbols,
+    uint32_t constellationType,
+    float sigma,
+    uint64_t seed,
+    uint64_t firstSymbolIndex,
+    int32_t cudaDevice,
+    hipStream_t cudaStream) GSDR_NO_EXCEPT;
+
 #endif /* GSDR_EXT_H_ */

@@ -424,3 +424,262 @@ void oracle_iir_f32(int cplx, const float* b, const float* a, size_t K, const fl
     free(ys);
   }
 }
+
+/* ---------------------------------------------------------------- A.6 the reference's decision rule */
+
+/* cuCabsf of CUDA's public cuComplex.h (the reference calls it at qpsk256.cu:173, 182); nvcc's default
+ * -fmad=true contracts `1.0f + t * t` into one fmaf. */
+float oracle_cuCabsf(float re, float im) {
+  const float a = fabsf(re), b = fabsf(im);
+  const float v = a > b ? a : b;
+  const float w = a > b ? b : a;
+  float t = w / v;
+  t = fmaf(t, t, 1.0f);
+  t = v * sqrtf(t);
+  if (v == 0.0f || v > 3.402823466e38f || w > 3.402823466e38f) t = v + w;
+  return t;
+}
+
+void oracle_qpsk256_demod_cuabs(const float* table, const float* in, uint8_t* out, uint32_t n) {
+  for (uint32_t k = 0; k < n; ++k) {
+    const float rx = in[2 * k], ry = in[2 * k + 1];
+    float best = INFINITY;
+    unsigned idx = 0;
+    for (unsigned i = 0; i < 256; ++i) {
+      /* cuCsubf(received, point), then cuCabsf (qpsk256.cu:172-177) */
+      const float d = oracle_cuCabsf(rx - table[2 * i], ry - table[2 * i + 1]);
+      if (d < best) {
+        best = d;
+        idx = i;
+      }
+    }
+    out[k] = (uint8_t)idx;
+  }
+}
+
+/* ---------------------------------------------------------------- config 5 channel: counter-based AWGN */
+
+void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+  uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3], k0 = key[0], k1 = key[1];
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n1 = (uint32_t)p1;
+    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1, n3 = (uint32_t)p0;
+    c0 = n0;
+    c1 = n1;
+    c2 = n2;
+    c3 = n3;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  out[0] = c0;
+  out[1] = c1;
+  out[2] = c2;
+  out[3] = c3;
+}
+
+static float f_from_bits(uint32_t b) {
+  float f;
+  memcpy(&f, &b, 4);
+  return f;
+}
+static uint32_t f_bits(float f) {
+  uint32_t b;
+  memcpy(&b, &f, 4);
+  return b;
+}
+
+/* ln u for u in (0, 1): u = m 2^e, m in [sqrt(1/2), sqrt(2)); ln m = 2 s P(s^2), s = (m - 1)/(m + 1) */
+static float awgn_log(float u) {
+  const uint32_t b = f_bits(u);
+  int e = (int)((b >> 23) & 0xffu) - 127;
+  float m = f_from_bits((b & 0x007fffffu) | 0x3f800000u);
+  if (m > 1.41421354f) {
+    m = m * 0.5f;
+    e += 1;
+  }
+  const float s = (m - 1.0f) / (m + 1.0f);
+  const float z = s * s;
+  float p = 0.09090909361839294f;
+  p = fmaf(p, z, 0.1111111119389534f);
+  p = fmaf(p, z, 0.1428571492433548f);
+  p = fmaf(p, z, 0.20000000298023224f);
+  p = fmaf(p, z, 0.3333333432674408f);
+  p = fmaf(p, z, 1.0f);
+  const float lnm = (2.0f * s) * p;
+  const float fe = (float)e;
+  return fmaf(fe, 0.693145751953125f, fmaf(fe, 1.428606765330187e-06f, lnm));
+}
+
+/* (cos, sin)(2 pi u) for u in [0, 1): quadrant q = floor(4u), f = 4u - q (both exact), polynomials in f
+ * for the angle f pi / 2 */
+static void awgn_sincos_turns(float u, float* c, float* s) {
+  const float u4 = u * 4.0f;
+  const int q = (int)u4;
+  const float f = u4 - (float)q;
+  const float z = f * f;
+  float sp = 5.6921727775716136e-08f;
+  sp = fmaf(sp, z, -3.598843250074424e-06f);
+  sp = fmaf(sp, z, 0.00016044118092395365f);
+  sp = fmaf(sp, z, -0.004681753925979137f);
+  sp = fmaf(sp, z, 0.07969262450933456f);
+  sp = fmaf(sp, z, -0.6459640860557556f);
+  sp = fmaf(sp, z, 1.5707963705062866f);
+  const float sn = sp * f;
+  float cp = -6.386603246255618e-09f;
+  cp = fmaf(cp, z, 4.710874748070637e-07f);
+  cp = fmaf(cp, z, -2.520204179745633e-05f);
+  cp = fmaf(cp, z, 0.0009192602592520416f);
+  cp = fmaf(cp, z, -0.020863480865955353f);
+  cp = fmaf(cp, z, 0.25366950035095215f);
+  cp = fmaf(cp, z, -1.2337005138397217f);
+  const float cs = fmaf(cp, z, 1.0f);
+  switch (q & 3) {
+    case 0: *c = cs; *s = sn; break;
+    case 1: *c = -sn; *s = cs; break;
+    case 2: *c = -cs; *s = -sn; break;
+    default: *c = sn; *s = -cs; break;
+  }
+}
+
+static void awgn_box_muller(uint32_t w0, uint32_t w1, float* g0, float* g1) {
+  const float u1 = ((float)(w0 >> 9) + 0.5f) * 1.1920928955078125e-07f; /* 2^-23 */
+  const float u2 = (float)(w1 >> 8) * 5.9604644775390625e-08f;          /* 2^-24 */
+  const float r = sqrtf(-2.0f * awgn_log(u1));
+  float c, s;
+  awgn_sincos_turns(u2, &c, &s);
+  *g0 = r * c;
+  *g1 = r * s;
+}
+
+void oracle_awgn_normals(uint64_t seed, uint64_t symbol_index, float* g0, float* g1) {
+  const uint64_t pair = symbol_index >> 1;
+  const uint32_t ctr[4] = {(uint32_t)pair, (uint32_t)(pair >> 32), 0u, 0u};
+  const uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+  uint32_t w[4];
+  oracle_philox4x32_10(ctr, key, w);
+  const int odd = (int)(symbol_index & 1u);
+  awgn_box_muller(w[2 * odd], w[2 * odd + 1], g0, g1);
+}
+
+void oracle_qpsk256_mod_awgn(const float* table, const uint8_t* in, float* out, uint32_t n, float sigma,
+                             uint64_t seed, uint64_t first_symbol) {
+  for (uint32_t k = 0; k < n; ++k) {
+    float g0, g1;
+    oracle_awgn_normals(seed, first_symbol + k, &g0, &g1);
+    out[2 * k] = table[2 * in[k]] + sigma * g0;
+    out[2 * k + 1] = table[2 * in[k] + 1] + sigma * g1;
+  }
+}
+
+/* ---------------------------------------------------------------- multi-threaded forms (CPU baseline) */
+
+typedef struct {
+  int kind;
+  size_t k0, k1;
+  size_t D, T;
+  const float* t;
+  const float* x;
+  float* y;
+  float fs, tune, chan, dev;
+  uint64_t n0;
+  const float* table;
+  const uint8_t* in8;
+  uint8_t* out8;
+  float sigma;
+  uint64_t seed, first;
+} RangeJob;
+
+static void* range_worker(void* arg) {
+  const RangeJob* j = (const RangeJob*)arg;
+  if (j->k1 <= j->k0) return NULL;
+  switch (j->kind) {
+    case 0:
+      oracle_fir_ff(j->D, j->t, j->T, j->x, j->y, j->k0, j->k1);
+      break;
+    case 1:
+      oracle_fm_demod(j->fs, j->tune, j->chan, j->dev, (uint32_t)j->D, j->n0, j->t, j->T, j->x, j->y, j->k0, j->k1);
+      break;
+    case 2:
+      oracle_qpsk256_demod(j->table, j->x + 2 * j->k0, j->out8 + j->k0, (uint32_t)(j->k1 - j->k0));
+      break;
+    case 3:
+      oracle_qpsk256_demod_cuabs(j->table, j->x + 2 * j->k0, j->out8 + j->k0, (uint32_t)(j->k1 - j->k0));
+      break;
+    default:
+      oracle_qpsk256_mod_awgn(j->table, j->in8 + j->k0, j->y + 2 * j->k0, (uint32_t)(j->k1 - j->k0), j->sigma,
+                              j->seed, j->first + j->k0);
+      break;
+  }
+  return NULL;
+}
+
+static void run_ranges(const RangeJob* proto, size_t m0, size_t m1, int nthreads) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  pthread_t th[256];
+  RangeJob jobs[256];
+  const size_t n = m1 - m0;
+  for (int w = 0; w < nthreads; ++w) {
+    jobs[w] = *proto;
+    jobs[w].k0 = m0 + n * (size_t)w / (size_t)nthreads;
+    jobs[w].k1 = m0 + n * (size_t)(w + 1) / (size_t)nthreads;
+  }
+  for (int w = 1; w < nthreads; ++w) pthread_create(&th[w], NULL, range_worker, &jobs[w]);
+  range_worker(&jobs[0]);
+  for (int w = 1; w < nthreads; ++w) pthread_join(th[w], NULL);
+}
+
+void oracle_fir_ff_mt(size_t D, const float* t, size_t T, const float* x, float* y, size_t N, int nthreads) {
+  RangeJob j;
+  memset(&j, 0, sizeof(j));
+  j.kind = 0;
+  j.D = D;
+  j.T = T;
+  j.t = t;
+  j.x = x;
+  j.y = y;
+  run_ranges(&j, 0, N, nthreads);
+}
+
+void oracle_fm_demod_mt(float fs, float tune, float chan, float dev, uint32_t D, uint64_t n0, const float* taps,
+                        size_t T, const float* x, float* out, size_t m0, size_t m1, int nthreads) {
+  RangeJob j;
+  memset(&j, 0, sizeof(j));
+  j.kind = 1;
+  j.fs = fs;
+  j.tune = tune;
+  j.chan = chan;
+  j.dev = dev;
+  j.D = D;
+  j.n0 = n0;
+  j.t = taps;
+  j.T = T;
+  j.x = x;
+  j.y = out;
+  run_ranges(&j, m0, m1, nthreads);
+}
+
+void oracle_qpsk256_demod_mt(int rule, const float* table, const float* in, uint8_t* out, uint32_t n, int nthreads) {
+  RangeJob j;
+  memset(&j, 0, sizeof(j));
+  j.kind = rule == 1 ? 3 : 2;
+  j.table = table;
+  j.x = in;
+  j.out8 = out;
+  run_ranges(&j, 0, n, nthreads);
+}
+
+void oracle_qpsk256_mod_awgn_mt(const float* table, const uint8_t* in, float* out, uint32_t n, float sigma,
+                                uint64_t seed, uint64_t first_symbol, int nthreads) {
+  RangeJob j;
+  memset(&j, 0, sizeof(j));
+  j.kind = 4;
+  j.table = table;
+  j.in8 = in;
+  j.y = out;
+  j.sigma = sigma;
+  j.seed = seed;
+  j.first = first_symbol;
+  run_ranges(&j, 0, n, nthreads);
+}

@@ -101,4 +101,34 @@ void oracle_iir(int cplx, const float* b, const float* a, size_t K, float* xh, f
 void oracle_iir_f32(int cplx, const float* b, const float* a, size_t K, const float* xh, const float* yh,
                     const float* x, float* y, size_t n);
 
+/* QPSK256 demodulation with the reference's literal rule (qpsk256.cu:171-181): first index of the
+ * minimum cuCabsf(received - point), strict <. cuCabsf restated from CUDA's public cuComplex.h
+ * (v = max(|a|, |b|), w = min, t = w / v, |z| = v * sqrtf(1 + t*t), v + w when v == 0 or either is
+ * beyond FLT_MAX), with `1 + t*t` contracted to fmaf(t, t, 1) as nvcc does by default (-fmad=true). */
+float oracle_cuCabsf(float re, float im);
+void oracle_qpsk256_demod_cuabs(const float* table, const float* in, uint8_t* out, uint32_t n);
+
+/* Config 5's channel (gsdrxQpsk256ModulateAwgn, include/gsdr/gsdr_ext.h): counter-based AWGN that the
+ * host reproduces bit for bit. Philox4x32-10 (Salmon et al., SC'11) keyed by the 64-bit seed, counter
+ * = (pair index lo, hi, 0, 0) with pair index = absolute symbol index >> 1; words (0,1) drive the even
+ * symbol of the pair, (2,3) the odd one. u1 = ((w0 >> 9) + 0.5) 2^-23 in (0, 1), u2 = (w1 >> 8) 2^-24
+ * in [0, 1); (g0, g1) = sqrt(-2 ln u1) (cos, sin)(2 pi u2) by Box-Muller, with ln, sin and cos
+ * evaluated by fixed polynomial sequences of IEEE +, -, *, /, sqrt and fmaf only (no libm), so the
+ * device and the host round identically. Output = table[s] + (sigma g0, sigma g1), each sum rounded
+ * once. */
+void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+void oracle_awgn_normals(uint64_t seed, uint64_t symbol_index, float* g0, float* g1);
+void oracle_qpsk256_mod_awgn(const float* table, const uint8_t* in, float* out, uint32_t n, float sigma,
+                             uint64_t seed, uint64_t first_symbol);
+
+/* Multi-threaded forms for the timed CPU baseline (static split of the output range over nthreads
+ * pthreads); each thread runs the scalar restatement above on its range. rule: 0 squared distance,
+ * 1 cuCabsf. */
+void oracle_fir_ff_mt(size_t D, const float* t, size_t T, const float* x, float* y, size_t N, int nthreads);
+void oracle_fm_demod_mt(float fs, float tune, float chan, float dev, uint32_t D, uint64_t n0, const float* taps,
+                        size_t T, const float* x, float* out, size_t m0, size_t m1, int nthreads);
+void oracle_qpsk256_demod_mt(int rule, const float* table, const float* in, uint8_t* out, uint32_t n, int nthreads);
+void oracle_qpsk256_mod_awgn_mt(const float* table, const uint8_t* in, float* out, uint32_t n, float sigma,
+                                uint64_t seed, uint64_t first_symbol, int nthreads);
+
 #endif /* GSDR_ORACLE_H_ */

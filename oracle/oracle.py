@@ -11,7 +11,10 @@ import os
 
 import numpy as np
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "build", "liboracle.so")
+# GSDR_ORACLE_LIB: another build of the same C source (bench.py's cpu_baseline builds one tuned for the
+# host it runs on); the default is the in-tree build.
+LIB_PATH = os.environ.get("GSDR_ORACLE_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "build",
+                                                             "liboracle.so")
 if not os.path.exists(LIB_PATH):
     raise ImportError(f"{LIB_PATH} missing: run `make oracle/build/liboracle.so`")
 _lib = ctypes.CDLL(LIB_PATH)
@@ -38,6 +41,14 @@ _SIG = {
     "oracle_qpsk256_mod": [_p, _p, _p, _u32],
     "oracle_qpsk256_demod": [_p, _p, _p, _u32],
     "oracle_qpsk256_demod_hypot": [_p, _p, _p, _u32],
+    "oracle_qpsk256_demod_cuabs": [_p, _p, _p, _u32],
+    "oracle_philox4x32_10": [_p, _p, _p],
+    "oracle_awgn_normals": [_u64, _u64, _p, _p],
+    "oracle_qpsk256_mod_awgn": [_p, _p, _p, _u32, _f, _u64, _u64],
+    "oracle_fir_ff_mt": [_sz, _p, _sz, _p, _p, _sz, _int],
+    "oracle_fm_demod_mt": [_f, _f, _f, _f, _u32, _u64, _p, _sz, _p, _p, _sz, _sz, _int],
+    "oracle_qpsk256_demod_mt": [_int, _p, _p, _p, _u32, _int],
+    "oracle_qpsk256_mod_awgn_mt": [_p, _p, _p, _u32, _f, _u64, _u64, _int],
     "oracle_add_const": [_int, _p, _f, _f, _p, _sz],
     "oracle_multiply": [_int, _p, _p, _p, _sz],
     "oracle_add_to_magnitude": [_p, _f, _p, _sz],
@@ -51,6 +62,8 @@ for _name, _args in _SIG.items():
     getattr(_lib, _name).argtypes = _args
     getattr(_lib, _name).restype = None
 _lib.oracle_nco_inc.argtypes = [_f, _f, _f]
+_lib.oracle_cuCabsf.argtypes = [_f, _f]
+_lib.oracle_cuCabsf.restype = _f
 _lib.oracle_nco_inc.restype = _u32
 
 
@@ -200,12 +213,67 @@ def qpsk256_mod(table, symbols):
     return out
 
 
-def qpsk256_demod(table, x, rule="sq"):
+def qpsk256_demod(table, x, rule="cuabs", nthreads=1):
+    """rule: "cuabs" the reference's cuCabsf rule (qpsk256.cu:171-181; the library's contract), "sq" the
+    squared distance (cross-check), "hypot" libm hypotf in place of cuCabsf."""
     table = _c(table, np.complex64)
     x = _c(x, np.complex64)
     out = np.empty(x.size, dtype=np.uint8)
-    fn = _lib.oracle_qpsk256_demod if rule == "sq" else _lib.oracle_qpsk256_demod_hypot
+    if nthreads > 1 and rule in ("sq", "cuabs"):
+        _lib.oracle_qpsk256_demod_mt(1 if rule == "cuabs" else 0, _ptr(table), _ptr(x), _ptr(out), x.size, nthreads)
+        return out
+    fn = {"sq": _lib.oracle_qpsk256_demod, "hypot": _lib.oracle_qpsk256_demod_hypot,
+          "cuabs": _lib.oracle_qpsk256_demod_cuabs}[rule]
     fn(_ptr(table), _ptr(x), _ptr(out), x.size)
+    return out
+
+
+def cuCabsf(re, im):
+    return float(_lib.oracle_cuCabsf(re, im))
+
+
+def philox4x32_10(ctr, key):
+    c = np.asarray(ctr, dtype=np.uint32)
+    k = np.asarray(key, dtype=np.uint32)
+    out = np.empty(4, dtype=np.uint32)
+    _lib.oracle_philox4x32_10(_ptr(c), _ptr(k), _ptr(out))
+    return out
+
+
+def awgn_normals(seed, symbol_index):
+    g0, g1 = ctypes.c_float(), ctypes.c_float()
+    _lib.oracle_awgn_normals(seed, symbol_index, ctypes.byref(g0), ctypes.byref(g1))
+    return g0.value, g1.value
+
+
+def qpsk256_mod_awgn(table, symbols, sigma, seed, first_symbol=0, nthreads=1):
+    """gsdrxQpsk256ModulateAwgn's contract: table[s] + sigma * counter-based Gaussian pair."""
+    table = _c(table, np.complex64)
+    symbols = _c(symbols, np.uint8)
+    out = np.empty(symbols.size, dtype=np.complex64)
+    if nthreads > 1:
+        _lib.oracle_qpsk256_mod_awgn_mt(_ptr(table), _ptr(symbols), _ptr(out), symbols.size, sigma, seed, first_symbol,
+                                        nthreads)
+    else:
+        _lib.oracle_qpsk256_mod_awgn(_ptr(table), _ptr(symbols), _ptr(out), symbols.size, sigma, seed, first_symbol)
+    return out
+
+
+def fir_ff_mt(taps, x, decimation, num_outputs, nthreads):
+    taps = _c(taps, np.float32)
+    x = _c(x, np.float32)
+    y = np.empty(num_outputs, dtype=np.float32)
+    _lib.oracle_fir_ff_mt(decimation, _ptr(taps), taps.size, _ptr(x), _ptr(y), num_outputs, nthreads)
+    return y
+
+
+def fm_demod_mt(x, taps, fs, tune, chan, dev, decimation, first_sample_index, num_outputs, nthreads, m0=0, m1=None):
+    x = _c(x, np.complex64)
+    taps = _c(taps, np.float32)
+    m1 = num_outputs if m1 is None else m1
+    out = np.zeros(num_outputs, dtype=np.float32)
+    _lib.oracle_fm_demod_mt(fs, tune, chan, dev, decimation, first_sample_index, _ptr(taps), taps.size, _ptr(x),
+                            _ptr(out), m0, m1, nthreads)
     return out
 
 

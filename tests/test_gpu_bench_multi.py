@@ -1,0 +1,44 @@
+"""GPU: the N > 1 bench path (BASELINE configs[3]: independent channels, one process per GPU, no
+data-path collective) run end to end as a fresh `torch.distributed.run` job with two ranks.
+
+On a one-GPU box the ranks share cuda:0 and talk over gloo (BENCH_REHEARSE=1, bench.py); the
+driver's 8-GPU run uses RCCL with one rank per GPU. The line must carry n_gpus = 2, the weak-scaling
+aggregate (both ranks' samples over the slowest rank's time) and the config-4 FM record. This is a
+rehearsal of the code path, not a scaling measurement."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_bench_two_ranks_rehearsal(cuda):
+    env = dict(os.environ, BENCH_REHEARSE="1", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "5", "--warmup", "2", "--settle-max", "50", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 prints exactly one JSON line
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["steps"] == 5 and line["scaling"] == "weak"
+    assert line["config"]["channels"] == 2 and "rehearsal" in line
+    # value = both ranks' input samples over the slowest rank's wall time
+    per_step_s = line["ms_per_step"] * 1e-3
+    want = 2 * line["config"]["input_samples"] / per_step_s / 1e6
+    assert abs(line["value"] - want) <= 0.01 * want
+    fm = line["secondary"]["fm_chain_multi_gpu"]
+    assert fm["n_gpus"] == 2 and fm["us_per_launch_max_over_ranks"] > 0
+    assert fm["aggregate_msamples_per_s"] > 0

@@ -75,7 +75,7 @@ def test_qpsk256_oracle_vs_golden(name, ctype):
     else:  # golden circular table uses float64 cos/sin rounded; oracle uses libm cosf/sinf
         assert np.max(np.abs(t - g["table"])) < 4e-7
     assert np.array_equal(o.qpsk256_mod(g["table"], g["symbols"]), g["tx"])
-    assert np.array_equal(o.qpsk256_demod(g["table"], g["rx"]), g["demod"])
+    assert np.array_equal(o.qpsk256_demod(g["table"], g["rx"], "sq"), g["demod"])
 
 
 # ---------------------------------------------------------------- reference known-answer tests

@@ -101,36 +101,118 @@ def measure_copy_peak(torch, device, nbytes=1 << 30, reps=10):
     return gbps
 
 
-def cpu_baseline(x_host, taps_np, threads):
-    """Time the C oracle (oracle/gsdr_oracle.c, scalar fmaf port of fir.cu:49-71) on this host."""
-    import numpy as np
+def host_cores():
+    """CPUs this process may use: its affinity mask, capped by a cgroup CPU quota when one is set (a GPU
+    box shares the machine, and its quota, not nproc, is what a CPU job gets). (count, how)."""
+    n = len(os.sched_getaffinity(0))
+    how = "sched_getaffinity"
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            q = max(1, int(-(-int(quota) // int(period))))
+            if q < n:
+                n, how = q, "cgroup cpu.max quota"
+    except (OSError, ValueError):
+        pass
+    return n, how
 
-    from oracle import oracle as orc
 
-    # repeated passes over the full channel until ~10 s of wall time (at least 3): median per pass
+def native_oracle():
+    """Build the C oracle for this host (-O3 -march=native, no contraction: the explicit fmaf calls stay
+    the only fused operations) into a temporary directory; fall back to the prebuilt in-tree build.
+    Returns the compile description. Must run before `oracle` is imported."""
+    import subprocess
+    import tempfile
+
+    src = os.path.join(ROOT, "oracle", "gsdr_oracle.c")
+    out = os.path.join(tempfile.mkdtemp(prefix="gsdr_oracle_"), "liboracle_native.so")
+    flags = ["-O3", "-march=native", "-std=c11", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math"]
+    try:
+        subprocess.run(["gcc"] + flags + ["-I", os.path.join(ROOT, "oracle"), src, "-o", out, "-lm", "-lpthread"],
+                       check=True, capture_output=True, timeout=120)
+        os.environ["GSDR_ORACLE_LIB"] = out
+        return "gcc " + " ".join(flags[:2] + flags[5:]) + " (built on this host)"
+    except (OSError, subprocess.SubprocessError):
+        return "prebuilt oracle/build/liboracle.so (gcc -O2 -mfma -ffp-contract=off)"
+
+
+def _timed(fn, min_s, min_reps=3):
+    """Median wall time of repeated fn() calls, repeated for at least min_s seconds."""
     times, t_start = [], time.perf_counter()
-    while len(times) < 3 or time.perf_counter() - t_start < CPU_SAMPLE_S:
+    while len(times) < min_reps or time.perf_counter() - t_start < min_s:
         t0 = time.perf_counter()
-        orc.fir_fc_mt(taps_np, x_host, DECIM, N_OUT, threads)
+        fn()
         times.append(time.perf_counter() - t0)
     times.sort()
-    med = times[len(times) // 2]
-    # single-thread rate on a 1/16 slice of the same workload
+    return times[len(times) // 2], len(times), sum(times)
+
+
+def cpu_baselines(x_host, taps_np, threads, c5):
+    """The C oracle (oracle/gsdr_oracle.c: scalar restatement of the reference kernels, one output per
+    loop iteration, split over `threads` pthreads by output range) timed on this host for BASELINE
+    configs 1, 2, 3 and 5, each on a bounded sample of its workload, with all cores and with one."""
+    import numpy as np
+
+    from gsdr_amd.signals import fm_test_signal, lowpass_taps
+    from oracle import oracle as orc
+
+    res = {}
+    # config 2 (the headline): repeated passes over the full channel, ~10 s
+    med, reps, tot = _timed(lambda: orc.fir_fc_mt(taps_np, x_host, DECIM, N_OUT, threads), CPU_SAMPLE_S)
     n1 = N_OUT // 16
     xs = np.ascontiguousarray(x_host[: (n1 - 1) * DECIM + TAPS])
-    t0 = time.perf_counter()
-    orc.fir_fc_mt(taps_np, xs, DECIM, n1, 1)
-    t1 = time.perf_counter() - t0
-    return {
-        "value": round(N_IN / med / 1e6, 2),
-        "unit": "Msamples/s",
-        "cores": threads,
-        "kind": "port",
-        "sample": f"{len(times)} passes over the full config-2 channel ({N_IN} input samples -> {N_OUT} outputs), "
-                  f"{sum(times):.1f} s of {threads}-thread work (static split by output range), median pass",
-        "best_msamples_per_s": round(N_IN / times[0] / 1e6, 2),
-        "single_thread_msamples_per_s": round(((n1 - 1) * DECIM + TAPS) / t1 / 1e6, 2),
-    }
+    one, _, _ = _timed(lambda: orc.fir_fc_mt(taps_np, xs, DECIM, n1, 1), 1.0, 1)
+    res["2"] = {"workload": "127-tap complex FIR, D = 4, 67,108,987 samples (gsdrFirFC)",
+                "value": round(N_IN / med / 1e6, 2), "unit": "Msamples/s",
+                "sample": f"{reps} passes over the full channel, {tot:.1f} s, median pass",
+                "single_thread": round(((n1 - 1) * DECIM + TAPS) / one / 1e6, 2)}
+    # config 1: 63-tap real FIR, no decimation, 1 M float samples
+    t63 = lowpass_taps(63, 0.1)
+    x1 = np.random.default_rng(1).uniform(-1, 1, 1 << 20).astype(np.float32)
+    nout1 = x1.size - 63 + 1
+    med, reps, tot = _timed(lambda: orc.fir_ff_mt(t63, x1, 1, nout1, threads), 2.0)
+    one, _, _ = _timed(lambda: orc.fir_ff_mt(t63, x1, 1, nout1, 1), 1.0, 2)
+    res["1"] = {"workload": "63-tap real FIR, no decimation, 1,048,576 float samples (gsdrFirFF)",
+                "value": round(x1.size / med / 1e6, 2), "unit": "Msamples/s",
+                "sample": f"{reps} passes over the full 1 M-sample input, {tot:.1f} s, median pass",
+                "single_thread": round(x1.size / one / 1e6, 2)}
+    # config 3: NCO + FIR + FM discriminator on config 3's signal; the oracle mixes every tap of every
+    # window as the reference's k_Fm does (fm.cu:40-63), so a 2^18-output slice of the channel
+    n3 = 1 << 18
+    x3 = fm_test_signal(n3 * DECIM + TAPS, noise=0.05, seed=0x5EED)
+    med, reps, tot = _timed(lambda: orc.fm_demod_mt(x3, taps_np, 1.0e6, 0.0, 1.0e5, 2.0e4, DECIM, 0, n3, threads),
+                            3.0)
+    one, _, _ = _timed(lambda: orc.fm_demod_mt(x3, taps_np, 1.0e6, 0.0, 1.0e5, 2.0e4, DECIM, 0, n3 // 16, 1), 1.0, 1)
+    res["3"] = {"workload": "NCO + 127-tap FIR (D = 4) + FM discriminator (gsdrFmDemod)",
+                "value": round(n3 * DECIM / med / 1e6, 2), "unit": "Msamples/s",
+                "sample": f"{n3} outputs ({n3 * DECIM + TAPS} samples) of config 3's signal, {reps} passes, "
+                          f"{tot:.1f} s, median pass",
+                "single_thread": round((n3 // 16) * DECIM / one / 1e6, 2)}
+    # config 5: modulate -> AWGN -> demodulate (reference cuCabsf rule, exhaustive 256-point search) on a
+    # 2^20-symbol slice of the GPU's symbols; the GPU's noisy symbols and decisions for that slice are
+    # checked against the oracle here (the full 2^24 round trip is tests/test_gpu_qpsk.py)
+    if c5 is not None:
+        table = orc.qpsk256_table(0, 1.0)
+        syms, rx_gpu, dec_gpu, sigma, seed = c5
+        k = syms.size
+
+        def round_trip():
+            rx = orc.qpsk256_mod_awgn(table, syms, sigma, seed, 0, nthreads=threads)
+            return rx, orc.qpsk256_demod(table, rx, nthreads=threads)
+
+        med, reps, tot = _timed(round_trip, 3.0)
+        rx, dec = round_trip()
+        t1 = time.perf_counter()
+        orc.qpsk256_demod(table, orc.qpsk256_mod_awgn(table, syms[: k // 16], sigma, seed, 0), nthreads=1)
+        one = time.perf_counter() - t1
+        res["5"] = {"workload": "QPSK256 rectangular modulate -> AWGN (sigma 0.02) -> demodulate",
+                    "value": round(k / med / 1e6, 2), "unit": "Msymbols/s",
+                    "sample": f"{k} symbols (the first of the GPU run's 2^24), {reps} passes, {tot:.1f} s, median",
+                    "single_thread": round((k // 16) / one / 1e6, 2),
+                    "gpu_noisy_symbols_bit_exact": bool(rx.tobytes() == rx_gpu.tobytes()),
+                    "gpu_decisions_bit_exact": bool(np.array_equal(dec, dec_gpu))}
+    return res
 
 
 def settle_clocks(torch, step, max_launches, window=25, tol=0.02):
@@ -293,6 +375,20 @@ def secondary_configs(torch, ops, device, taps):
             "us_per_launch": round(t * 1e6, 2), "msamples_per_s": round(n / t / 1e6, 1),
             "alg_gbps": round(2 * nbytes * n / t / 1e9, 1)}
         del xi, yi
+    # config 1 (BASELINE configs[0]: the reference's CPU-runnable case) on the GPU: 63-tap real FIR, no
+    # decimation, 1 M float samples -- one launch is a few microseconds, so launch overhead dominates
+    from gsdr_amd.signals import lowpass_taps
+
+    x1 = torch.rand(1 << 20, device=device, generator=g) * 2 - 1
+    t63 = torch.from_numpy(lowpass_taps(63, 0.1)).to(device)
+    n1 = x1.numel() - 63 + 1
+    y1 = torch.empty(n1, dtype=torch.float32, device=device)
+    argsets = [(1, t63.data_ptr(), 63, x1.data_ptr(), y1.data_ptr(), n1, device.index, stream)]
+    t = time_abi(torch, abi.lib.gsdrFirFF, argsets, reps=200, settle=100)
+    out["fir_ff_config1"] = {"config": "BASELINE configs[0]: 63-tap real FIR (gsdrFirFF), no decimation, 1,048,576 "
+                                       "float samples", "us_per_launch": round(t * 1e6, 2),
+                             "msamples_per_s": round(x1.numel() / t / 1e6, 1)}
+    del x1, y1
     reps = 50
     n = 1 << 24
     ops.qpsk256_init(0, 1.0, device.index)
@@ -318,7 +414,29 @@ def secondary_configs(torch, ops, device, taps):
     out["qpsk256"] = {"config": "QPSK256 rectangular, 2^24 symbols, AWGN sigma 0.02/axis",
                       "modulate_us": round(tm * 1e6, 2), "demodulate_us": round(td * 1e6, 2),
                       "alg_gbps_mod": round(9 * n / tm / 1e9, 1), "alg_gbps_demod": round(9 * n / td / 1e9, 1),
-                      "ser": round(float((rx_bytes != syms).float().mean()), 6)}
+                      "ser": round(float((rx_bytes != syms).float().mean()), 6),
+                      "decision_rule": "reference cuCabsf argmin (qpsk256.cu:171-181), bit-exact"}
+    # BASELINE configs[4] as specified: modulate + counter-based AWGN fused (gsdrxQpsk256ModulateAwgn),
+    # then demodulate; the noise is host-reproducible (the cpu_baseline leg checks a slice)
+    sigma, seed = 0.02, 0x5EED0005
+    for _ in range(2):
+        ops.qpsk256_modulate_awgn(syms, 0, sigma, seed, 0, out=tx)
+    s4, e4 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s4.record()
+    for _ in range(reps):
+        ops.qpsk256_modulate_awgn(syms, 0, sigma, seed, 0, out=tx)
+    e4.record()
+    torch.cuda.synchronize()
+    ta = s4.elapsed_time(e4) / reps * 1e-3
+    ops.qpsk256_demodulate(tx, 0, out=rx_bytes)
+    torch.cuda.synchronize()
+    out["qpsk256"]["modulate_awgn_us"] = round(ta * 1e6, 2)
+    out["qpsk256"]["round_trip_us"] = round((ta + td) * 1e6, 2)
+    out["qpsk256"]["round_trip_msymbols_per_s"] = round(n / (ta + td) / 1e6, 1)
+    out["qpsk256"]["ser_awgn"] = round(float((rx_bytes != syms).float().mean()), 6)
+    out["qpsk256"]["squared_distance_rule_disagreements"] = sq_rule_disagreements(torch, tx, 0)
+    k5 = 1 << 20
+    c5 = (syms[:k5].cpu().numpy(), tx[:k5].cpu().numpy(), rx_bytes[:k5].cpu().numpy(), sigma, seed)
     # circular table (per-cell candidate lists), same symbols, sigma 0.01/axis
     ops.qpsk256_init(1, 1.0, device.index)
     ops.qpsk256_modulate(syms, 1, out=tx)
@@ -333,7 +451,26 @@ def secondary_configs(torch, ops, device, taps):
     tc = s3.elapsed_time(e3) / reps * 1e-3
     out["qpsk256"]["demodulate_circular_us"] = round(tc * 1e6, 2)
     out["qpsk256"]["ser_circular_sigma_0.01"] = round(float((rx_bytes != syms).float().mean()), 6)
-    return out
+    return out, c5
+
+
+def sq_rule_disagreements(torch, rx, ctype, chunk=1 << 19):
+    """Symbols (of rx) whose squared-distance argmin differs from the library's decision rule, the
+    reference's cuCabsf argmin: how often the two rules part (near-ties only). Counted with torch on
+    the GPU: d = (rx - c)^2 summed per axis in float32, first index of the minimum."""
+    from gsdr_amd import ops
+
+    table = ops.qpsk256_modulate(torch.arange(256, dtype=torch.uint8, device=rx.device), ctype)
+    dec = ops.qpsk256_demodulate(rx, ctype)
+    tr, ti = table.real[None, :], table.imag[None, :]
+    n = 0
+    for k in range(0, rx.numel(), chunk):
+        r = rx[k:k + chunk]
+        dx = r.real[:, None] - tr
+        dy = r.imag[:, None] - ti
+        d = dx * dx + dy * dy
+        n += int((torch.argmin(d, dim=1).to(torch.uint8) != dec[k:k + chunk]).sum())
+    return n
 
 
 def main():
@@ -483,13 +620,33 @@ def main():
         line["roofline"]["frac_of_measured_copy"] = round(achieved / cp, 4)
     except RuntimeError:
         pass
+    c5 = None
     if world == 1 and not args.no_secondary:
-        line["secondary"] = secondary_configs(torch, ops, device, taps)
+        line["secondary"], c5 = secondary_configs(torch, ops, device, taps)
     if fm_multi is not None:
         line["secondary"] = {"fm_chain_multi_gpu": fm_multi}
     if world == 1 and not args.no_cpu_baseline:
-        threads = min(16, os.cpu_count() or 1)
-        line["cpu_baseline"] = cpu_baseline(x.cpu().numpy(), taps_np, threads)
+        threads, how = host_cores()
+        build = native_oracle()
+        per = cpu_baselines(x.cpu().numpy(), taps_np, threads, c5)
+        gpu = {"2": N_IN / kern_s / 1e6}
+        sec = line.get("secondary", {})
+        if "fir_ff_config1" in sec:
+            gpu["1"] = sec["fir_ff_config1"]["msamples_per_s"]
+        if "fm_chain" in sec:
+            gpu["3"] = sec["fm_chain"]["msamples_per_s"]
+        if "qpsk256" in sec:
+            gpu["5"] = sec["qpsk256"]["round_trip_msymbols_per_s"]
+        for k, v in per.items():
+            v["cores"] = threads
+            if k in gpu:
+                v["gpu_value"] = round(gpu[k], 1)
+                v["gpu_over_cpu"] = round(gpu[k] / v["value"], 1)
+        c2 = per["2"]
+        line["cpu_baseline"] = {"value": c2["value"], "unit": "Msamples/s", "cores": threads, "kind": "port",
+                                "sample": c2["sample"] + " (config 2; configs 1, 3, 5 under `configs`)",
+                                "cores_source": how, "build": build,
+                                "single_thread_msamples_per_s": c2["single_thread"], "configs": per}
     print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -8,7 +8,7 @@
 //     words (0, 1) belong to the even symbol of the pair, (2, 3) to the odd one.
 //   * u1 = ((w0 >> 9) + 0.5) 2^-23 in (0, 1), u2 = (w1 >> 8) 2^-24 in [0, 1), both exact in float.
 //   * Box-Muller: (g0, g1) = sqrt(-2 ln u1) (cos, sin)(2 pi u2), with ln, cos and sin evaluated by
-//     fixed sequences of correctly rounded IEEE operations (+, -, *, __fdiv_rn, __fsqrt_rn, fmaf) --
+//     fixed sequences of correctly rounded IEEE operations (+, -, *, /, sqrt, fmaf) --
 //     no hardware transcendental, no libm -- so the host restatement (oracle/gsdr_oracle.c) rounds
 //     identically. ln: u = m 2^e, m in [sqrt(1/2), sqrt(2)), ln m = 2 s P(s^2), s = (m - 1)/(m + 1);
 //     sin/cos: quadrant q = floor(4 u2), f = 4 u2 - q, odd/even Taylor polynomials of f pi / 2 (errors
@@ -47,7 +47,7 @@ __device__ __forceinline__ float awgn_log(float u) {
     m = m * 0.5f;
     e += 1;
   }
-  const float s = __fdiv_rn(m - 1.0f, m + 1.0f);
+  const float s = (m - 1.0f) / (m + 1.0f);  // correctly rounded: HIP's default f32 division
   const float z = s * s;
   float p = 0.09090909361839294f;
   p = fmaf(p, z, 0.1111111119389534f);
@@ -92,7 +92,9 @@ __device__ __forceinline__ float2 awgn_cos_sin_turns(float u) {
 __device__ __forceinline__ float2 awgn_box_muller(uint32_t w0, uint32_t w1) {
   const float u1 = ((float)(w0 >> 9) + 0.5f) * 1.1920928955078125e-07f;  // 2^-23
   const float u2 = (float)(w1 >> 8) * 5.9604644775390625e-08f;           // 2^-24
-  const float r = __fsqrt_rn(-2.0f * awgn_log(u1));
+  // __builtin_sqrtf is the correctly rounded IEEE square root (HIP's default); __fsqrt_rn is NOT: in
+  // this toolchain it maps to __ocml_native_sqrt_f32 (the ~1-ulp hardware v_sqrt_f32).
+  const float r = __builtin_sqrtf(-2.0f * awgn_log(u1));
   const float2 cs = awgn_cos_sin_turns(u2);
   return make_float2(r * cs.x, r * cs.y);
 }

@@ -69,14 +69,15 @@ __device__ __forceinline__ float sqdist(float2 r, float2 c) {
 
 // cuCabsf (CUDA cuComplex.h, called at qpsk256.cu:173, 182): v = max(|a|, |b|), w = min, t = w / v,
 // |z| = v * sqrt(fma(t, t, 1)), v + w when v == 0 or either exceeds FLT_MAX. IEEE division and square
-// root, as nvcc's defaults (-prec-div, -prec-sqrt) give.
+// root, as nvcc's defaults (-prec-div, -prec-sqrt) give: '/' and __builtin_sqrtf are correctly rounded
+// under HIP's defaults (__fsqrt_rn is not: this toolchain maps it to the ~1-ulp v_sqrt_f32).
 __device__ __forceinline__ float ref_cabsf(float re, float im) {
   const float a = fabsf(re), b = fabsf(im);
   const float v = a > b ? a : b;
   const float w = a > b ? b : a;
   float t = __fdiv_rn(w, v);
   t = fmaf(t, t, 1.0f);
-  t = __fmul_rn(v, __fsqrt_rn(t));
+  t = __fmul_rn(v, __builtin_sqrtf(t));
   if (v == 0.0f || v > 3.402823466e38f || w > 3.402823466e38f) t = __fadd_rn(v, w);
   return t;
 }

@@ -209,10 +209,18 @@ __device__ __forceinline__ float2 nco_direct(uint32_t phase) {
   return make_float2(__builtin_amdgcn_cosf(r), __builtin_amdgcn_sinf(r));
 }
 
-// a * b with explicit fmas (pk_mul + pk_fma; the library builds with -ffp-contract=off, so the
-// rounding is fixed here rather than left to the contraction pass)
+// a * b with explicit fmas: (fma(a.x, b.x, -(a.y b.y)), fma(a.x, b.y, a.y b.x)). Written on
+// two-lane vectors so it is exactly one v_pk_mul_f32 (a.y * (-b.y, b.x), the sign as a neg_lo source
+// modifier) and one v_pk_fma_f32 (a.x * b + that); the library builds with -ffp-contract=off, so the
+// rounding is fixed here rather than left to the contraction pass.
+typedef float gsdr_f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
-  return make_float2(fmaf(a.x, b.x, -(a.y * b.y)), fmaf(a.x, b.y, a.y * b.x));
+  const gsdr_f32x2 bv = gsdr_f32x2{b.x, b.y};
+  // (-b.y, b.x) as b swapped times (-1, 1) (exact): one v_pk_mul_f32, where building it with a sign flip
+  // and a move took two instructions
+  const gsdr_f32x2 t = gsdr_f32x2{a.y, a.y} * (bv.yx * gsdr_f32x2{-1.0f, 1.0f});
+  const gsdr_f32x2 r = __builtin_elementwise_fma(gsdr_f32x2{a.x, a.x}, bv, t);
+  return make_float2(r.x, r.y);
 }
 
 // phasor of absolute sample n (low 32 bits suffice: P is taken mod 2^32)
@@ -450,6 +458,11 @@ __device__ __forceinline__ void stage_tile(float4* __restrict__ lds, const InT* 
       return;
     }
   }
+  // The body loop, instantiated once per NCO start parity (`odd` is uniform over the tile): with the
+  // parity a runtime value the compiler kept a branch around every granule's phasor.
+  const uint32_t pbase = Geo::padded(tid);
+  auto body = [&](auto odd_c) {
+    constexpr bool ODD = decltype(odd_c)::value;
 #pragma unroll
   for (int b0 = 0; b0 < BPT; b0 += SB) {
     float4 v[SB];
@@ -483,9 +496,19 @@ __device__ __forceinline__ void stage_tile(float4* __restrict__ lds, const InT* 
 #pragma unroll
     for (int k = 0; k < SB; ++k) {
       const uint32_t g = (b0 + k) * WG + tid;
-      lds[Geo::padded(g)] =
-          stage_transform_ph<InT, MODE, NODIRECT>(v[k], pw.ph0 + (uint32_t)(b0 + k) * pw.step, pw.odd, pw.inc);
+      // padded(k * WG + tid) = padded(tid) + k * padded(WG) when whole segments fit a workgroup's row of
+      // granules: a per-thread base plus an immediate offset per granule
+      const uint32_t slot = (WG % Geo::SG == 0) ? pbase + (uint32_t)(b0 + k) * Geo::padded(WG) : Geo::padded(g);
+      lds[slot] = stage_transform_ph<InT, MODE, NODIRECT>(v[k], pw.ph0 + (uint32_t)(b0 + k) * pw.step, ODD, pw.inc);
     }
+  }
+  };
+  if constexpr (MODE == kModeFir) {
+    body(std::false_type{});
+  } else if (pw.odd) {
+    body(std::true_type{});
+  } else {
+    body(std::false_type{});
   }
   for (uint32_t g = BPT * WG + tid; g < NG; g += WG) {
     const uint64_t s = S0 + (uint64_t)g * G;
@@ -538,32 +561,70 @@ __device__ __forceinline__ void store_fir(OutT* __restrict__ out, uint64_t k0, u
 // src/quad_demod.cu:30-31).
 // atan2 for the discriminators: octant reduction t = min/max (v_rcp_f32), an odd minimax polynomial
 // for atan on [0, 1] (max abs error 3.3e-7 rad in float32 evaluation, tools/atan_fit.py), then the
-// octant fix-ups. Zeros, infinities and NaN take the library atan2f, so its special values
+// octant fix-ups. Outside 2^-100 < |x| + |y| < 2^100 (zeros, infinities, NaN, and magnitudes where
+// v_rcp_f32 would leave the normal range) the library atan2f is used, so its special values
 // (atan2(0, 0) = 0, atan2(+-0, -0) = +-pi, ...) are unchanged. The discriminator bar is 3.1e-5 rad
 // (1e-5 of pi; tests/helpers.py wrapped_angle_err).
-__device__ __forceinline__ float disc_atan2(float y, float x) {
-  const float ax = fabsf(x), ay = fabsf(y);
-  const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
-  if (!(ax < INFINITY && ay < INFINITY) || mx == 0.0f) return atan2f(y, x);
-  const float t = mn * __builtin_amdgcn_rcpf(mx);
-  const float s = t * t;
-  float p = 0.006811787374317646f;
-  p = fmaf(p, s, -0.0336042121052742f);
-  p = fmaf(p, s, 0.07962368428707123f);
-  p = fmaf(p, s, -0.132333442568779f);
-  p = fmaf(p, s, 0.19807817041873932f);
-  p = fmaf(p, s, -0.3331736922264099f);
-  p = fmaf(p, s, 0.9999961256980896f);
-  float r = p * t;
-  if (ay > ax) r = 1.57079637f - r;
+// The scalar form (disc_atan2 / fm_disc) and the two-at-a-time form (fm_disc2, packed FMAs) run the
+// same IEEE operations in the same order, so every kernel's discriminator outputs are bit-identical.
+__device__ __forceinline__ bool disc_fast(float y, float x) {
+  const float s = fabsf(x) + fabsf(y);
+  return s > 0x1p-100f && s < 0x1p100f;
+}
+
+__device__ __forceinline__ gsdr_f32x2 atan_poly2(gsdr_f32x2 t) {
+  const gsdr_f32x2 s = t * t;
+  gsdr_f32x2 p = __builtin_elementwise_fma(gsdr_f32x2{0.006811787374317646f, 0.006811787374317646f}, s,
+                                           gsdr_f32x2{-0.0336042121052742f, -0.0336042121052742f});
+  p = __builtin_elementwise_fma(p, s, gsdr_f32x2{0.07962368428707123f, 0.07962368428707123f});
+  p = __builtin_elementwise_fma(p, s, gsdr_f32x2{-0.132333442568779f, -0.132333442568779f});
+  p = __builtin_elementwise_fma(p, s, gsdr_f32x2{0.19807817041873932f, 0.19807817041873932f});
+  p = __builtin_elementwise_fma(p, s, gsdr_f32x2{-0.3331736922264099f, -0.3331736922264099f});
+  p = __builtin_elementwise_fma(p, s, gsdr_f32x2{0.9999961256980896f, 0.9999961256980896f});
+  return p * t;
+}
+
+// octant fix-ups of the polynomial result r = atan(min/max) for (y, x)
+__device__ __forceinline__ float disc_octant(float r, float y, float x) {
+  if (fabsf(y) > fabsf(x)) r = 1.57079637f - r;
   if (x < 0.0f) r = 3.14159274f - r;
   return copysignf(r, y);
 }
 
+__device__ __forceinline__ float disc_atan2(float y, float x) {
+  if (!disc_fast(y, x)) return atan2f(y, x);
+  const float ax = fabsf(x), ay = fabsf(y);
+  const float t = fminf(ax, ay) * __builtin_amdgcn_rcpf(fmaxf(ax, ay));
+  return disc_octant(atan_poly2(gsdr_f32x2{t, t}).x, y, x);
+}
+
+__device__ __forceinline__ float2 disc_product(float2 y0, float2 y1) {
+  return make_float2(y1.x * y0.x + y1.y * y0.y, y1.y * y0.x - y1.x * y0.y);
+}
+
 __device__ __forceinline__ float fm_disc(float2 y0, float2 y1, float g) {
-  const float re = y1.x * y0.x + y1.y * y0.y;
-  const float im = y1.y * y0.x - y1.x * y0.y;
-  return g * disc_atan2(im, re);
+  const float2 z = disc_product(y0, y1);
+  return g * disc_atan2(z.y, z.x);
+}
+
+// fm_disc(a0, a1) and fm_disc(b0, b1) with the polynomial, the fix-up subtractions and the gain on
+// packed FMAs / multiplies (two outputs per instruction)
+__device__ __forceinline__ gsdr_f32x2 fm_disc2(float2 a0, float2 a1, float2 b0, float2 b1, float g) {
+  const float2 za = disc_product(a0, a1), zb = disc_product(b0, b1);
+  const float axa = fabsf(za.x), aya = fabsf(za.y), axb = fabsf(zb.x), ayb = fabsf(zb.y);
+  const gsdr_f32x2 t = gsdr_f32x2{fminf(axa, aya), fminf(axb, ayb)} *
+                       gsdr_f32x2{__builtin_amdgcn_rcpf(fmaxf(axa, aya)), __builtin_amdgcn_rcpf(fmaxf(axb, ayb))};
+  gsdr_f32x2 r = atan_poly2(t);
+  const gsdr_f32x2 q = gsdr_f32x2{1.57079637f, 1.57079637f} - r;
+  r.x = aya > axa ? q.x : r.x;
+  r.y = ayb > axb ? q.y : r.y;
+  const gsdr_f32x2 h = gsdr_f32x2{3.14159274f, 3.14159274f} - r;
+  r.x = za.x < 0.0f ? h.x : r.x;
+  r.y = zb.x < 0.0f ? h.y : r.y;
+  r = gsdr_f32x2{copysignf(r.x, za.y), copysignf(r.y, zb.y)};
+  if (!disc_fast(za.y, za.x)) r.x = atan2f(za.y, za.x);
+  if (!disc_fast(zb.y, zb.x)) r.y = atan2f(zb.y, zb.x);
+  return gsdr_f32x2{g, g} * r;
 }
 
 // AM envelope: 2 * saturate(|y|) - 1, saturate(NaN) = 0 (reference src/am.cu:49, quad_demod.cu:47-48).
@@ -605,9 +666,11 @@ __device__ __forceinline__ bool store_tile_lds(float4* lds, const FirParams& p, 
   return true;
 }
 
-// Shared by both tiled kernels. `xs` is a WG-sized LDS exchange area (FM mode only).
-template <int MODE, class OutT, int R, int WG, bool NTS = false>
-__device__ __forceinline__ void tile_epilogue(const FirParams& p, uint64_t out0, OutT (&acc)[R], float2* xs) {
+// Shared by the tiled kernels. `xs` is a WG-sized LDS exchange area (FM mode only); `tile` the staged
+// input tile, which FM mode with COAL reuses (WG * R floats) once every wave is done with it.
+template <int MODE, class OutT, int R, int WG, bool NTS = false, bool COAL = false>
+__device__ __forceinline__ void tile_epilogue(const FirParams& p, uint64_t out0, OutT (&acc)[R], float2* xs,
+                                              float4* tile = nullptr) {
   const uint32_t t = threadIdx.x;
   const uint32_t local0 = t * R;
   if constexpr (MODE == kModeFir) {
@@ -628,13 +691,37 @@ __device__ __forceinline__ void tile_epilogue(const FirParams& p, uint64_t out0,
     // scratch when R = 1
     const float2 nb = xs[t + 1 < WG ? t + 1 : t];
     const float2 nxt = (t + 1 < WG) ? nb : acc[R - 1];
-    float* out = reinterpret_cast<float*>(p.out);
+    float o[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const float2 y1 = (r + 1 < R) ? acc[r + 1] : nxt;
-      const uint32_t ml = local0 + r;
-      const uint64_t m = out0 + ml;
-      if (ml < p.tile_stride && m < p.N) out[m] = fm_disc(acc[r], y1, p.fm_gain);
+    for (int r = 0; r + 1 < R; r += 2) {
+      const float2 y2 = (r + 2 < R) ? acc[r + 2] : nxt;
+      const gsdr_f32x2 v = fm_disc2(acc[r], acc[r + 1], acc[r + 1], y2, p.fm_gain);
+      o[r] = v.x;
+      o[r + 1] = v.y;
+    }
+    if constexpr (R % 2 == 1) o[R - 1] = fm_disc(acc[R - 1], nxt, p.fm_gain);
+    float* out = reinterpret_cast<float*>(p.out);
+    if constexpr (COAL && R > 1) {
+      // Through LDS so that every wave instruction stores one contiguous 256-byte run: stored
+      // straight from registers, a thread's R outputs put the lanes of one dword store R * 4 bytes
+      // apart. The tile area is free: every wave has passed the barrier above, i.e. finished its MACs.
+      float* lo = reinterpret_cast<float*>(tile);
+#pragma unroll
+      for (int r = 0; r < R; ++r) lo[local0 + r] = o[r];
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < R; ++q) {
+        const uint32_t ml = q * WG + t;
+        const uint64_t m = out0 + ml;
+        if (ml < p.tile_stride && m < p.N) out[m] = lo[ml];
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const uint32_t ml = local0 + r;
+        const uint64_t m = out0 + ml;
+        if (ml < p.tile_stride && m < p.N) out[m] = o[r];
+      }
     }
   }
 }
@@ -765,7 +852,6 @@ __device__ __forceinline__ void ascending_fixup(const float4* __restrict__ lds, 
 // Inf term makes it NaN or Inf). A finite set whose sum overflows only sends the thread through the
 // per-output test in the fix-up, which then changes nothing. Packed adds: 5 VALU operations for R = 4
 // complex outputs instead of one class test per component.
-typedef float gsdr_f32x2 __attribute__((ext_vector_type(2)));
 template <int R>
 __device__ __forceinline__ bool all_finite(const float2 (&acc)[R]) {
   gsdr_f32x2 s = {acc[0].x, acc[0].y};
@@ -856,7 +942,7 @@ __global__ __launch_bounds__(WG) void k_fir_poly(FirParams p) {
     return;
   }
   float2* xs = reinterpret_cast<float2*>(lds + Geo::padded(NG - 1) + 1);
-  tile_epilogue<MODE, OutT, R, WG, NT>(p, out0, acc, xs);
+  tile_epilogue<MODE, OutT, R, WG, NT, true>(p, out0, acc, xs, lds);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -922,10 +1008,18 @@ __global__ __launch_bounds__(WG) void k_fir_multi(FirParams p, MultiParams mp) {
     pc.fm_gain = mp.gain[c];
     pc.out = reinterpret_cast<float*>(p.out) + (uint64_t)c * p.N;
     const PhaseWalk pw = phase_walk<G, WG>(p.nco_n0, S0, pc.nco_inc);
+    auto mix = [&](auto odd_c) {  // one instantiation per (tile-uniform) NCO start parity, as stage_tile
 #pragma unroll
-    for (int k = 0; k < BPT; ++k) {
-      const uint32_t g = k * WG + tid;
-      lds[Geo::padded(g)] = stage_transform_ph<InT, MODE>(body[k], pw.ph0 + (uint32_t)k * pw.step, pw.odd, pw.inc);
+      for (int k = 0; k < BPT; ++k) {
+        const uint32_t g = k * WG + tid;
+        lds[Geo::padded(g)] =
+            stage_transform_ph<InT, MODE>(body[k], pw.ph0 + (uint32_t)k * pw.step, decltype(odd_c)::value, pw.inc);
+      }
+    };
+    if (pw.odd) {
+      mix(std::true_type{});
+    } else {
+      mix(std::false_type{});
     }
 #pragma unroll
     for (int k = 0; k < HMAX; ++k) {

@@ -415,13 +415,16 @@ __global__ __launch_bounds__(TileShape<S>::WG) void k_iir_chunks(Coeffs cf, cons
       float* __restrict__ row = reinterpret_cast<float*>(tile + (t / NC) * TSh::STRIDE) + comp;
       // inputs held as doubles (converted once per sample, exact); a whole chunk is fully unrolled
       // so the state shifts are register renames
+      // The feedback terms are added oldest first, so only the last FMA (a[1] y[n-1]) waits for the
+      // previous step's output: one FMA latency per sample on the recursion's critical path instead of
+      // P (the chunk passes are latency-bound).
       auto step = [&](uint32_t k) {
         const double xv = (double)row[k * NC];
         double acc = b[0] * xv;
 #pragma unroll
         for (int i = 1; i <= P; ++i) acc = fma(b[i], xd[i - 1], acc);
 #pragma unroll
-        for (int i = 1; i <= P; ++i) acc = fma(am[i], ys[i - 1], acc);
+        for (int i = P; i >= 1; --i) acc = fma(am[i], ys[i - 1], acc);
 #pragma unroll
         for (int i = P - 1; i > 0; --i) {
           xd[i] = xd[i - 1];

@@ -13,7 +13,7 @@ SRCS := $(wildcard gsdr_amd/csrc/*.hip)
 HDRS := $(wildcard gsdr_amd/csrc/*.hpp) $(wildcard include/gsdr/*.h)
 OBJS := $(patsubst gsdr_amd/csrc/%.hip,$(BUILD)/%.o,$(SRCS))
 
-all: gsdr_amd/libgsdr.so oracle/build/liboracle.so examples
+all: gsdr_amd/libgsdr.so oracle/build/liboracle.so examples probes
 
 $(BUILD)/%.o: gsdr_amd/csrc/%.hip $(HDRS)
 	@mkdir -p $(BUILD)

@@ -259,6 +259,31 @@ def time_abi(torch, fn, argsets, reps=50, settle=400):
     return s.elapsed_time(e) / reps * 1e-3
 
 
+PROBES_LIB = os.path.join(ROOT, "build", "probes", "libgsdr_probes.so")
+
+
+def staging_ceiling(torch, xs, y, taps, dev_index, stream):
+    """The headline kernel with its FIR MACs removed (tuning-probe variant 107 of the separate probes
+    build: the same tiles, non-temporal HBM -> LDS staging and output stores, no multiply-adds), timed
+    the same way on the same buffers. Its byte rate is what this traffic mix can stream on this box;
+    the FIR's achieved rate over it says how much of the gap to 8 TB/s is the arithmetic (the power cap,
+    DESIGN.md section 3.1). None when the probes library was not built."""
+    if not os.path.exists(PROBES_LIB):
+        return None
+    import ctypes
+
+    lib = ctypes.CDLL(PROBES_LIB)
+    fn = lib.gsdrxFirFCVariant
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p,
+                   ctypes.c_size_t, ctypes.c_int32, ctypes.c_void_p]
+    out = {}
+    for v, name in ((107, "staging_only"), (104, "compute_only")):
+        argsets = [(v, DECIM, taps.data_ptr(), TAPS, xb.data_ptr(), y.data_ptr(), N_OUT, dev_index, stream) for xb in xs]
+        out[name] = time_abi(torch, fn, argsets, reps=100, settle=600)
+    return out
+
+
 def fm_channel(torch, n, device, seed, n0=0):
     """Config 3's input generated on the device: constant-envelope FM, carrier +0.1 fs,
     message tone 0.001 fs, peak deviation 0.02 fs, amplitude 1, plus AWGN sigma 0.05 per axis; samples
@@ -620,6 +645,18 @@ def main():
         line["roofline"]["frac_of_measured_copy"] = round(achieved / cp, 4)
     except RuntimeError:
         pass
+    if world == 1 and not args.no_secondary:
+        ceil = staging_ceiling(torch, xs, y, taps, dev_index, stream)
+        if ceil is not None:
+            st_gbps = ALG_BYTES / ceil["staging_only"] / 1e9
+            line["roofline"]["staging_ceiling"] = {
+                "gbps": round(st_gbps, 1),
+                "us": round(ceil["staging_only"] * 1e6, 2),
+                "frac_of_ceiling": round(achieved / st_gbps, 4),
+                "compute_only_us": round(ceil["compute_only"] * 1e6, 2),
+                "source": "probes build (make probes), gsdrxFirFCVariant 107: this kernel's staging and stores "
+                          "without the multiply-adds; 104: the multiply-adds without the staging",
+            }
     c5 = None
     if world == 1 and not args.no_secondary:
         line["secondary"], c5 = secondary_configs(torch, ops, device, taps)

@@ -14,9 +14,9 @@
  *   Modulate   (qpsk256.cu:74-101):  output[k] = point_type[input[k]]; `amplitude` is ignored, the scale is
  *                                     fixed by InitConstellation (as in the reference).
  *   Demodulate (qpsk256.cu:154-195): output[k] = the first index i attaining the minimum of
- *                                     d_i = fl(fl(dx*dx) + fl(dy*dy)), dx = re - point_i.re, dy = im - point_i.im
- *                                     (squared distance in place of cuCabsf: same argmin, bit-exact between
- *                                     CPU and GPU); a non-finite received symbol yields 0 as in the reference.
+ *                                     cuCabsf(input[k] - point_i) (qpsk256.cu:171-181; CUDA's cuCabsf with IEEE
+ *                                     division and square root), bit for bit; a non-finite received symbol
+ *                                     yields 0 as in the reference.
  */
 #ifndef GSDR_QPSK256_H_
 #define GSDR_QPSK256_H_

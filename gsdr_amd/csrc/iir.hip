@@ -218,7 +218,10 @@ constexpr bool kTableInLds = kGroup * P * P * sizeof(double) <= 32 * 1024;
 // Level-0 scan fused into the chunk passes (P <= kFusedMaxP): the tails pass runs the up-sweep of its
 // own groups from LDS (no tails round trip through HBM, no separate launch) and the final pass
 // derives each chunk's start state itself (the level-0 down-sweep).
-constexpr int kFusedMaxP = 8;
+#ifndef IIR_FUSED_MAXP
+#define IIR_FUSED_MAXP 8
+#endif
+constexpr int kFusedMaxP = IIR_FUSED_MAXP;
 
 struct ScanArgs {
   double* incl;          // level-0 inclusive zero-state prefixes (A[P] per chunk); tails pass writes

@@ -296,10 +296,8 @@ __global__ __launch_bounds__(TileShape<S>::WG) void k_iir_chunks(Coeffs cf, cons
       return;
     }
   }
-  // Workgroup b filters tiles b, b + nwg, ... (the launcher starts one workgroup per tile; a
-  // register prefetch of the next tile in a persistent grid measured no faster). Barriers wait for
-  // LDS only (lds_barrier), so global loads issued before them stay in flight.
-  const uint32_t nwg = PASS == kTails ? gridDim.x - 1 : gridDim.x;
+  // Workgroup b filters tile b (a register prefetch of the next tile in a persistent grid measured no
+  // faster). Barriers wait for LDS only (lds_barrier), so global loads issued before them stay in flight.
   const uint64_t ntiles = (n + TSh::TS - 1) / TSh::TS;
   constexpr int SPV = 16 / sizeof(S);          // samples per 16-byte load
   constexpr int NV = TSh::TS / SPV / TSh::WG;   // 16-byte loads per thread for a whole tile
@@ -346,12 +344,16 @@ __global__ __launch_bounds__(TileShape<S>::WG) void k_iir_chunks(Coeffs cf, cons
     am[i] = -coeff(cf.a, cf.K, i);
   }
   double* __restrict__ tails_d = reinterpret_cast<double*>(tails);
-  for (; ti < ntiles; ti += nwg) {
+  // One tile per workgroup (the launcher starts ntiles workgroups): written as a loop that ends after its
+  // first pass, so nothing is live across iterations. With `ti += nwg` the compiler kept the coefficients
+  // and the fused scan's state live around the loop: 148 VGPRs, 3 waves per SIMD, instead of 66 / 112.
+  for (; ti < ntiles; ti = ntiles) {
     const uint64_t base = ti * TSh::TS;
     const uint32_t tlen = n - base < (uint64_t)TSh::TS ? (uint32_t)(n - base) : (uint32_t)TSh::TS;
     const bool whole = is_whole(ti);
     float4 v[NV];
     if (whole) load_tile(ti, v);  // in flight while the final pass computes the chunk start state
+
     // the P samples before the tile (the input history for the first tile), loaded beside it
     S pv = zero_s(S{});
     if (t < P) pv = x_at(x, xh, cf.K, (int64_t)base - 1 - t);
@@ -666,7 +668,9 @@ static hipError_t run(const Coeffs& cf, S* xh, S* yh, const S* x, S* y, uint64_t
   const int Pk = K - 1;  // live state components (<= P); the rest stay zero
 
   constexpr int WG = TileShape<S>::WG;
-  const uint32_t blocks = (uint32_t)ceil_div<uint64_t>(n, TileShape<S>::TS);
+  const uint64_t ntiles = ceil_div<uint64_t>(n, TileShape<S>::TS);
+  if (ntiles >= 0x7fffffffull) return hipErrorInvalidValue;  // one workgroup per tile (k_iir_chunks)
+  const uint32_t blocks = (uint32_t)ntiles;
   const SetupArgs sa{yh, s0, table(0), levels};
   const bool vec = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15u) == 0;
   constexpr bool F = P <= kFusedMaxP;

@@ -574,12 +574,14 @@ __global__ __launch_bounds__(64) void k_iir_down(uint64_t E, const double* __res
   down_group<A, P>(E, T, group_starts, nullptr, incl_starts, blockIdx.x, threadIdx.x);
 }
 
-// The upper levels with at most kRestWaves groups run in one workgroup (one wave per group, a barrier
-// between levels, workgroup-scope visibility); larger levels get one launch each (a single workgroup
-// walking many groups serially is latency-bound).
+// The upper levels with at most kRestGroups groups run in ONE single-workgroup launch, up-sweeps then
+// down-sweeps (one wave per group, a barrier between levels, workgroup-scope visibility); larger levels
+// get one launch each. A single workgroup is latency-bound walking many groups: 128 groups per level
+// took 5x longer than a launch per level, and even with each wave scanning 4-8 groups at once (their
+// loads issued together) the whole of levels 1..3 for 2^24 samples took 72 us on one CU against ~19 us
+// for the per-level launches. Up and down in one launch: 8.9 us instead of 6.2 + 4.9 us.
 constexpr int kRestWaves = 16;
-constexpr int kRestGroups = 16;  // levels with at most this many groups go to the single-workgroup kernels
-                                 // (128 measured 5x slower: one workgroup walking 8 groups per wave is latency-bound)
+constexpr int kRestGroups = 16;
 template <class A>
 struct Levels {
   A* elems[kMaxLevels + 1];
@@ -590,26 +592,19 @@ struct Levels {
 };
 
 template <class A, int P>
-__global__ __launch_bounds__(64 * kRestWaves) void k_iir_up_rest(Levels<A> L, int first) {
+__global__ __launch_bounds__(64 * kRestWaves) void k_iir_scan_rest(Levels<A> L, const A* __restrict__ s0, int first) {
   const int w = threadIdx.x / 64, r = threadIdx.x % 64;
   for (int k = first; k <= L.levels; ++k) {
-    const double* T = L.T[k];
     const uint64_t groups = ceil_div<uint64_t>(L.E[k], kGroup);
     for (uint64_t g = w; g < groups; g += kRestWaves) {
-      up_group<A, P>(L.elems[k], L.E[k], T, L.starts[k], k < L.levels ? L.elems[k + 1] : nullptr, g, r);
+      up_group<A, P>(L.elems[k], L.E[k], L.T[k], L.starts[k], k < L.levels ? L.elems[k + 1] : nullptr, g, r);
     }
     __syncthreads();
   }
-}
-
-template <class A, int P>
-__global__ __launch_bounds__(64 * kRestWaves) void k_iir_down_rest(Levels<A> L, const A* __restrict__ s0, int lowest) {
-  const int w = threadIdx.x / 64, r = threadIdx.x % 64;
-  for (int k = L.levels; k >= lowest; --k) {
-    const double* T = L.T[k];
+  for (int k = L.levels; k >= first; --k) {
     const uint64_t groups = ceil_div<uint64_t>(L.E[k], kGroup);
     for (uint64_t g = w; g < groups; g += kRestWaves) {
-      down_group<A, P>(L.E[k], T, k < L.levels ? L.starts[k + 1] : nullptr, s0, L.starts[k], g, r);
+      down_group<A, P>(L.E[k], L.T[k], k < L.levels ? L.starts[k + 1] : nullptr, s0, L.starts[k], g, r);
     }
     __syncthreads();
   }
@@ -684,7 +679,7 @@ static hipError_t run(const Coeffs& cf, S* xh, S* yh, const S* x, S* y, uint64_t
     k_iir_chunks<S, P, kTails, false, F><<<blocks + 1, WG, 0, st>>>(cf, x, xh, n, nullptr, elems(0), nullptr, sa,
                                                                     up_args);
   }
-  // levels with more than kRestWaves groups: one launch each; the rest: one single-workgroup launch
+  // levels with more than kRestGroups groups: one launch each; the rest: one single-workgroup launch
   Levels<A> L{};
   for (int k = 0; k <= levels; ++k) {
     L.elems[k] = elems(k);
@@ -700,10 +695,7 @@ static hipError_t run(const Coeffs& cf, S* xh, S* yh, const S* x, S* y, uint64_t
     k_iir_up<A, P><<<(uint32_t)ceil_div<uint64_t>(E[k], kGroup), 64, 0, st>>>(elems(k), E[k], table(k), starts(k),
                                                                              elems(k + 1));
   }
-  if (rest <= levels) {
-    k_iir_up_rest<A, P><<<1, 64 * kRestWaves, 0, st>>>(L, rest);
-    k_iir_down_rest<A, P><<<1, 64 * kRestWaves, 0, st>>>(L, s0, rest);
-  }
+  if (rest <= levels) k_iir_scan_rest<A, P><<<1, 64 * kRestWaves, 0, st>>>(L, s0, rest);
   for (int k = rest - 1; k >= lowest; --k) {
     k_iir_down<A, P><<<(uint32_t)ceil_div<uint64_t>(E[k], kGroup), 64, 0, st>>>(E[k], table(k), starts(k + 1),
                                                                                starts(k));

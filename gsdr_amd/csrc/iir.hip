@@ -289,8 +289,9 @@ __global__ __launch_bounds__(TileShape<S>::WG) void k_iir_chunks(Coeffs cf, cons
   A* tl = reinterpret_cast<A*>(smem);  // fused tails pass: the chunk tails, once the tile is consumed
   const int t = threadIdx.x;
   if constexpr (PASS == kTails) {
-    // the extra last workgroup builds the scan constants while the others compute the tails
-    if (blockIdx.x == gridDim.x - 1) {
+    // the extra FIRST workgroup builds the scan constants while the others compute the tails (as the
+    // last one it was dispatched after most tiles and finished after them: ~7 us at the kernel's end)
+    if (blockIdx.x == 0) {
       iir_setup<S, P, TSh::WG, kTableInLds<P>>(cf, static_cast<const S*>(setup.yh), static_cast<A*>(setup.s0), setup.T,
                                                setup.levels, reinterpret_cast<double*>(smem));
       return;
@@ -309,7 +310,8 @@ __global__ __launch_bounds__(TileShape<S>::WG) void k_iir_chunks(Coeffs cf, cons
 #pragma unroll
     for (int k = 0; k < NV; ++k) r[k] = src[k * TSh::WG + t];
   };
-  uint64_t ti = blockIdx.x;
+  uint64_t ti = PASS == kTails ? blockIdx.x - 1 : blockIdx.x;
+  const uint64_t first_ti = ti;
   auto build_pow = [&]() {
     // M_0 (column j = state after kChunk steps of the homogeneous recursion from e_j), then squared:
     // the same operations as iir_setup's T[1], T[2], ..., T[32], so the same doubles
@@ -461,7 +463,7 @@ __global__ __launch_bounds__(TileShape<S>::WG) void k_iir_chunks(Coeffs cf, cons
       }
     }
     if constexpr (PASS == kTails && FUSED) {
-      if (ti == blockIdx.x) build_pow();
+      if (ti == first_ti) build_pow();
       lds_barrier();  // every lane is done reading the tile
       if (n0 < n) {
 #pragma unroll

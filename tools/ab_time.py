@@ -6,7 +6,7 @@ clock settle (untimed launches) and then 100 launches inside one HIP event pair.
 per build and workload, and whether outputs equal the first build's bit for bit.
 
     python tools/ab_time.py [other_lib.so ...]     (the in-tree gsdr_amd/libgsdr.so is always first)
-    AB_WORK=fir,fm  AB_ROUNDS=3
+    AB_WORK=fir,fm,fm16  AB_ROUNDS=3   (fm16: gsdrxFmDemodMulti, 16 channels, time per launch)
 """
 import ctypes
 import os
@@ -47,6 +47,10 @@ def main():
         if "fir8" in work else []
     yc = torch.empty(N, dtype=torch.complex64, device=dev)
     yf = torch.empty(N, dtype=torch.float32, device=dev)
+    nch = 16
+    ym = torch.empty(nch * (N - 1), dtype=torch.float32, device=dev) if "fm16" in work else yf
+    chans = (ctypes.c_float * nch)(*[CHAN - 3.0e4 * k for k in range(nch)])
+    devs = (ctypes.c_float * nch)(*([DEV] * nch))
     F, U32, SZ, P, I32 = ctypes.c_float, ctypes.c_uint32, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int32
     specs = {
         "fir": ("gsdrFirFC", [SZ, P, SZ, P, P, SZ, I32, P], yc,
@@ -56,6 +60,9 @@ def main():
                xs),
         "am": ("gsdrAmDemod", [F, F, F, U32, SZ, P, SZ, P, P, SZ, I32, P], yf,
                lambda x: (FS, TUNE, CHAN, D, 0, taps.data_ptr(), T, x.data_ptr(), yf.data_ptr(), N, 0, stream), xs),
+        "fm16": ("gsdrxFmDemodMulti", [F, F, P, P, U32, U32, SZ, P, SZ, ctypes.c_int, P, P, SZ, I32, P], ym,
+                 lambda x: (FS, TUNE, ctypes.cast(chans, P), ctypes.cast(devs, P), nch, D, 0, taps.data_ptr(), T, 0,
+                            x.data_ptr(), ym.data_ptr(), N - 1, 0, stream), xs),
         "fir8": ("gsdrxFirFCInt8", [SZ, P, SZ, P, P, SZ, I32, P], yc,
                  lambda x: (D, taps.data_ptr(), T, x.data_ptr(), yc.data_ptr(), N, 0, stream), x8),
     }

@@ -4,13 +4,17 @@
 // The noise of absolute symbol k is a pure function of (seed, k), so the host can regenerate the exact
 // noisy buffer a launch produced (tests compare the full 2^24-symbol round trip against the CPU
 // oracle) and any split of a buffer into launches yields the same samples:
-//   * Philox4x32-10 (Salmon, Moraes, Dror, Shaw, SC'11): key = seed, counter = (k >> 1 lo, hi, 0, 0);
-//     words (0, 1) belong to the even symbol of the pair, (2, 3) to the odd one.
-//   * u1 = ((w0 >> 9) + 0.5) 2^-23 in (0, 1), u2 = (w1 >> 8) 2^-24 in [0, 1), both exact in float.
+//   * Philox4x32-10 (Salmon, Moraes, Dror, Shaw, SC'11): key = seed, counter = (k / 3 lo, hi, 0, 0);
+//     one 128-bit block serves three symbols (slot k % 3), 39 bits each (awgn_slot_bits):
+//     slot 0: a = w0 >> 9, b = w3 & 0xffff; slot 1: a = w1 >> 9, b = w3 >> 16;
+//     slot 2: a = w2 >> 9, b = (w0 & 0x1ff) << 7 | (w1 & 0x7f).
+//   * u1 = (a + 0.5) 2^-23 in (0, 1), u2 = b 2^-16 in [0, 1), both exact in float (u2 quantises the
+//     angle to 2^-16 turn; drawing 47 bits a symbol instead cost 50 % more Philox blocks, which bound
+//     the kernel).
 //   * Box-Muller: (g0, g1) = sqrt(-2 ln u1) (cos, sin)(2 pi u2), with ln, cos and sin evaluated by
-//     fixed sequences of correctly rounded IEEE operations (+, -, *, /, sqrt, fmaf) --
-//     no hardware transcendental, no libm -- so the host restatement (oracle/gsdr_oracle.c) rounds
-//     identically. ln: u = m 2^e, m in [sqrt(1/2), sqrt(2)), ln m = 2 s P(s^2), s = (m - 1)/(m + 1);
+//     fixed sequences of correctly rounded IEEE operations (+, -, *, sqrt, fmaf) -- no hardware
+//     transcendental, no libm -- so the host restatement (oracle/gsdr_oracle.c) rounds
+//     identically. ln: u = m 2^e, m in [sqrt(1/2), sqrt(2)), ln m = t q(t), t = m - 1 (degree-8 q);
 //     sin/cos: quadrant q = floor(4 u2), f = 4 u2 - q, odd/even Taylor polynomials of f pi / 2 (errors
 //     below 2e-7). Tails are cut at sqrt(-2 ln 2^-24) = 5.8 sigma.
 #pragma once
@@ -48,15 +52,19 @@ __device__ __forceinline__ float awgn_log(float u) {
     m = m * 0.5f;
     e += 1;
   }
-  const float s = (m - 1.0f) / (m + 1.0f);  // correctly rounded: HIP's default f32 division
-  const float z = s * s;
-  float p = 0.09090909361839294f;
-  p = fmaf(p, z, 0.1111111119389534f);
-  p = fmaf(p, z, 0.1428571492433548f);
-  p = fmaf(p, z, 0.20000000298023224f);
-  p = fmaf(p, z, 0.3333333432674408f);
-  p = fmaf(p, z, 1.0f);
-  const float lnm = (2.0f * s) * p;
+  /* ln m = t q(t), t = m - 1 in [sqrt(1/2) - 1, sqrt(2) - 1]: degree-8 q fitted on Chebyshev nodes,
+     max abs error 4.8e-8 in float32 Horner evaluation (no division) */
+  const float t = m - 1.0f;
+  float p = 0.08743945509195328f;
+  p = fmaf(p, t, -0.14377330243587494f);
+  p = fmaf(p, t, 0.14949095249176025f);
+  p = fmaf(p, t, -0.16560696065425873f);
+  p = fmaf(p, t, 0.19956977665424347f);
+  p = fmaf(p, t, -0.2500215470790863f);
+  p = fmaf(p, t, 0.3333418369293213f);
+  p = fmaf(p, t, -0.49999988079071045f);
+  p = fmaf(p, t, 1.0f);
+  const float lnm = p * t;
   const float fe = (float)e;
   return fmaf(fe, 0.693145751953125f, fmaf(fe, 1.428606765330187e-06f, lnm));
 }
@@ -90,9 +98,10 @@ __device__ __forceinline__ float2 awgn_cos_sin_turns(float u) {
   }
 }
 
-__device__ __forceinline__ float2 awgn_box_muller(uint32_t w0, uint32_t w1) {
-  const float u1 = ((float)(w0 >> 9) + 0.5f) * 1.1920928955078125e-07f;  // 2^-23
-  const float u2 = (float)(w1 >> 8) * 5.9604644775390625e-08f;           // 2^-24
+// a: 23 bits for u1, b: 16 bits for u2
+__device__ __forceinline__ float2 awgn_box_muller(uint32_t a, uint32_t b) {
+  const float u1 = ((float)a + 0.5f) * 1.1920928955078125e-07f;  // 2^-23
+  const float u2 = (float)b * 1.52587890625e-05f;                 // 2^-16
   // __builtin_sqrtf is the correctly rounded IEEE square root (HIP's default); __fsqrt_rn is NOT: in
   // this toolchain it maps to __ocml_native_sqrt_f32 (the ~1-ulp hardware v_sqrt_f32).
   const float r = __builtin_sqrtf(-2.0f * awgn_log(u1));
@@ -100,9 +109,16 @@ __device__ __forceinline__ float2 awgn_box_muller(uint32_t w0, uint32_t w1) {
   return make_float2(r * cs.x, r * cs.y);
 }
 
-// The Philox words of the pair holding absolute symbol k.
-__device__ __forceinline__ void awgn_pair_words(uint64_t seed, uint64_t pair, uint32_t (&w)[4]) {
-  philox4x32_10((uint32_t)pair, (uint32_t)(pair >> 32), 0u, 0u, (uint32_t)seed, (uint32_t)(seed >> 32), w);
+// The Philox block holding absolute symbols 3 blk .. 3 blk + 2.
+__device__ __forceinline__ void awgn_block_words(uint64_t seed, uint64_t blk, uint32_t (&w)[4]) {
+  philox4x32_10((uint32_t)blk, (uint32_t)(blk >> 32), 0u, 0u, (uint32_t)seed, (uint32_t)(seed >> 32), w);
+}
+
+// The normal pair of slot `slot` (0..2, compile-time after unrolling) of a block.
+__device__ __forceinline__ float2 awgn_slot(const uint32_t (&w)[4], int slot) {
+  if (slot == 0) return awgn_box_muller(w[0] >> 9, w[3] & 0xffffu);
+  if (slot == 1) return awgn_box_muller(w[1] >> 9, w[3] >> 16);
+  return awgn_box_muller(w[2] >> 9, ((w[0] & 0x1ffu) << 7) | (w[1] & 0x7fu));
 }
 
 }  // namespace gsdr

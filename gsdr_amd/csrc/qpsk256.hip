@@ -209,48 +209,46 @@ __global__ __launch_bounds__(kCBlock) void k_c256_mod(C256Streams st, uint32_t n
   }
 }
 
-// Modulate + counter-based AWGN (gsdrxQpsk256ModulateAwgn; awgn.hpp). Lane t of slot q handles the
-// local symbol pair q * kCBlock + t of the block (coalesced byte-pair loads and 16-byte stores, as
-// k_c256_mod). With an even first absolute index a local pair is one Philox pair (one call for two
-// symbols); with an odd one its symbols straddle two Philox pairs (two calls).
+// Modulate + counter-based AWGN (gsdrxQpsk256ModulateAwgn; awgn.hpp). One Philox block serves three
+// symbols, so a lane takes six consecutive symbols a step: two blocks when the first absolute index is a
+// multiple of 3 (R3 = firstSymbolIndex % 3, uniform, a template parameter so every slot and block index
+// is a compile-time constant), three otherwise. Three 16-byte stores a lane (48-byte lane stride).
+constexpr int kAwgnSym = 6;    // symbols per lane per step
+constexpr int kAwgnSteps = 3;  // steps per workgroup
+constexpr uint32_t kAwgnBlockSyms = kCBlock * kAwgnSym * kAwgnSteps;
+
+template <int R3>
 __global__ __launch_bounds__(kCBlock) void k_c256_mod_awgn(const uint8_t* __restrict__ in, float2* __restrict__ out,
                                                             uint32_t n, uint32_t type, float sigma, uint64_t seed,
                                                             uint64_t first) {
   __shared__ float2 tab[256];
   load_table(tab, type);
-  const bool odd0 = (first & 1u) != 0;
-  const uint64_t base = (uint64_t)blockIdx.x * kCBlock * kCSym;
-#pragma unroll 2
-  for (int q = 0; q < kCSym / 2; ++q) {
-    const uint64_t s = base + 2u * ((uint64_t)q * kCBlock + threadIdx.x);  // local symbol of the pair
+  constexpr int NB = R3 == 0 ? 2 : 3;  // Philox blocks touched by six symbols starting at slot R3
+  const uint64_t base = (uint64_t)blockIdx.x * kAwgnBlockSyms;
+#pragma unroll 1
+  for (int it = 0; it < kAwgnSteps; ++it) {
+    const uint64_t s = base + (uint64_t)kAwgnSym * ((uint32_t)it * kCBlock + threadIdx.x);  // local first symbol
     if (s >= n) break;
-    const bool two = s + 1 < n;
-    const uint64_t a = first + s;  // absolute index of the first symbol
-    uint32_t w[4];
-    awgn_pair_words(seed, a >> 1, w);
-    float2 g0, g1;
-    if (!odd0) {
-      g0 = awgn_box_muller(w[0], w[1]);
-      g1 = awgn_box_muller(w[2], w[3]);
-    } else {
-      g0 = awgn_box_muller(w[2], w[3]);
-      uint32_t w2[4];
-      awgn_pair_words(seed, (a + 1) >> 1, w2);
-      g1 = awgn_box_muller(w2[0], w2[1]);
+    const uint64_t b0 = (first + s) / 3u;  // (first + s) % 3 == R3: s is a multiple of 6
+    uint32_t w[NB][4];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) awgn_block_words(seed, b0 + b, w[b]);
+    float2 y[kAwgnSym];
+#pragma unroll
+    for (int j = 0; j < kAwgnSym; ++j) {
+      const float2 g = awgn_slot(w[(R3 + j) / 3], (R3 + j) % 3);
+      const float2 p = s + j < n ? tab[in[s + j]] : make_float2(0.0f, 0.0f);
+      y[j] = make_float2(p.x + sigma * g.x, p.y + sigma * g.y);
     }
-    const float2 p0 = tab[in[s]];
-    const float2 y0 = make_float2(p0.x + sigma * g0.x, p0.y + sigma * g0.y);
-    if (two) {
-      const float2 p1 = tab[in[s + 1]];
-      const float2 y1 = make_float2(p1.x + sigma * g1.x, p1.y + sigma * g1.y);
-      if ((reinterpret_cast<uintptr_t>(out + s) & 15u) == 0) {
-        *reinterpret_cast<float4*>(out + s) = make_float4(y0.x, y0.y, y1.x, y1.y);
-      } else {
-        out[s] = y0;
-        out[s + 1] = y1;
-      }
+    if (s + kAwgnSym <= n && (reinterpret_cast<uintptr_t>(out + s) & 15u) == 0) {
+      float4* o = reinterpret_cast<float4*>(out + s);
+#pragma unroll
+      for (int q = 0; q < kAwgnSym / 2; ++q) o[q] = make_float4(y[2 * q].x, y[2 * q].y, y[2 * q + 1].x, y[2 * q + 1].y);
     } else {
-      out[s] = y0;
+#pragma unroll
+      for (int j = 0; j < kAwgnSym; ++j) {
+        if (s + j < n) out[s + j] = y[j];
+      }
     }
   }
 }
@@ -588,10 +586,22 @@ GSDR_C_LINKAGE hipError_t gsdrxQpsk256ModulateAwgn(const uint8_t* inputBytes, hi
   }
   gsdr::DeviceScope scope(cudaDevice);
   if (scope.status() != hipSuccess) return scope.status();
-  const uint32_t blocks =
-      (uint32_t)gsdr::ceil_div<uint64_t>(gsdr::ceil_div<uint64_t>(numSymbols, gsdr::kCSym), gsdr::kCBlock);
-  gsdr::k_c256_mod_awgn<<<dim3(blocks), dim3(gsdr::kCBlock), 0, cudaStream>>>(
-      inputBytes, reinterpret_cast<float2*>(output), numSymbols, constellationType, sigma, seed, firstSymbolIndex);
+  const uint32_t blocks = (uint32_t)gsdr::ceil_div<uint64_t>(numSymbols, gsdr::kAwgnBlockSyms);
+  float2* out = reinterpret_cast<float2*>(output);
+  switch (firstSymbolIndex % 3u) {
+    case 0:
+      gsdr::k_c256_mod_awgn<0><<<dim3(blocks), dim3(gsdr::kCBlock), 0, cudaStream>>>(
+          inputBytes, out, numSymbols, constellationType, sigma, seed, firstSymbolIndex);
+      break;
+    case 1:
+      gsdr::k_c256_mod_awgn<1><<<dim3(blocks), dim3(gsdr::kCBlock), 0, cudaStream>>>(
+          inputBytes, out, numSymbols, constellationType, sigma, seed, firstSymbolIndex);
+      break;
+    default:
+      gsdr::k_c256_mod_awgn<2><<<dim3(blocks), dim3(gsdr::kCBlock), 0, cudaStream>>>(
+          inputBytes, out, numSymbols, constellationType, sigma, seed, firstSymbolIndex);
+      break;
+  }
   return gsdr::launch_status();
 }
 

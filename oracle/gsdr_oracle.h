@@ -110,10 +110,11 @@ void oracle_qpsk256_demod_cuabs(const float* table, const float* in, uint8_t* ou
 
 /* Config 5's channel (gsdrxQpsk256ModulateAwgn, include/gsdr/gsdr_ext.h): counter-based AWGN that the
  * host reproduces bit for bit. Philox4x32-10 (Salmon et al., SC'11) keyed by the 64-bit seed, counter
- * = (pair index lo, hi, 0, 0) with pair index = absolute symbol index >> 1; words (0,1) drive the even
- * symbol of the pair, (2,3) the odd one. u1 = ((w0 >> 9) + 0.5) 2^-23 in (0, 1), u2 = (w1 >> 8) 2^-24
- * in [0, 1); (g0, g1) = sqrt(-2 ln u1) (cos, sin)(2 pi u2) by Box-Muller, with ln, sin and cos
- * evaluated by fixed polynomial sequences of IEEE +, -, *, /, sqrt and fmaf only (no libm), so the
+ * = (block lo, hi, 0, 0) with block = absolute symbol index / 3; slot k % 3 takes 23 bits a and 16 bits
+ * b of the block's words w0..w3 (slot 0: w0 >> 9, w3 & 0xffff; slot 1: w1 >> 9, w3 >> 16; slot 2:
+ * w2 >> 9, (w0 & 0x1ff) << 7 | (w1 & 0x7f)); u1 = (a + 0.5) 2^-23 in (0, 1), u2 = b 2^-16 in [0, 1);
+ * (g0, g1) = sqrt(-2 ln u1) (cos, sin)(2 pi u2) by Box-Muller, with ln, sin and cos
+ * evaluated by fixed polynomial sequences of IEEE +, -, *, sqrt and fmaf only (no libm), so the
  * device and the host round identically. Output = table[s] + (sigma g0, sigma g1), each sum rounded
  * once. */
 void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);

@@ -27,11 +27,12 @@ def test_philox_known_answers(ctr, key, want):
 
 
 def _ref_normals(seed, k):
-    pair = k >> 1
-    w = o.philox4x32_10([pair & 0xffffffff, pair >> 32, 0, 0], [seed & 0xffffffff, seed >> 32])
-    w0, w1 = int(w[2 * (k & 1)]), int(w[2 * (k & 1) + 1])
-    u1 = ((w0 >> 9) + 0.5) * 2.0 ** -23
-    u2 = (w1 >> 8) * 2.0 ** -24
+    blk, slot = divmod(k, 3)  # three symbols per Philox block, 39 bits each (gsdr_amd/csrc/awgn.hpp)
+    w = [int(v) for v in o.philox4x32_10([blk & 0xffffffff, blk >> 32, 0, 0], [seed & 0xffffffff, seed >> 32])]
+    a, b = [(w[0] >> 9, w[3] & 0xffff), (w[1] >> 9, w[3] >> 16),
+            (w[2] >> 9, ((w[0] & 0x1ff) << 7) | (w[1] & 0x7f))][slot]
+    u1 = (a + 0.5) * 2.0 ** -23
+    u2 = b * 2.0 ** -16
     r = math.sqrt(-2.0 * math.log(u1))
     return r * math.cos(2 * math.pi * u2), r * math.sin(2 * math.pi * u2)
 

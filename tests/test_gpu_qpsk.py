@@ -190,11 +190,12 @@ def test_qpsk256_config5_round_trip(cuda, ctype, sigma):
     assert np.array_equal(got.cpu().numpy(), o.qpsk256_demod(table, rx_np, nthreads=_threads()))
 
 
-@pytest.mark.parametrize("n", [1, 2, 3, 4095, 4096, 4097, 100_003])
-@pytest.mark.parametrize("first", [0, 1, 2**32 - 1, 2**40 + 6])
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 6, 7, 1535, 1537, 4607, 4608, 4609, 100_003])  # 6 a lane step, 4608 a workgroup
+@pytest.mark.parametrize("first", [0, 1, 2, 2**32 - 1, 2**40 + 6, 2**33 + 3])  # first % 3: 0, 1, 2, 0, 1, 2
 def test_qpsk256_awgn_sizes_and_offsets(cuda, n, first):
-    """Every size, even and odd first absolute index (Philox pairs straddling the buffer), indices past
-    2^32; a buffer split over two calls equals one call."""
+    """Every size, every residue of the first absolute index mod 3 (a Philox block serves three symbols,
+    so blocks straddle the buffer's ends), indices past 2^32; a buffer split over two calls equals one
+    call."""
     from gsdr_amd import ops
 
     ctype, sigma, seed = 1, 0.05, 0xFEEDFACE12345678

@@ -217,7 +217,8 @@ constexpr bool kTableInLds = kGroup * P * P * sizeof(double) <= 32 * 1024;
 
 // Level-0 scan fused into the chunk passes (P <= kFusedMaxP): the tails pass runs the up-sweep of its
 // own groups from LDS (no tails round trip through HBM, no separate launch) and the final pass
-// derives each chunk's start state itself (the level-0 down-sweep).
+// derives each chunk's start state itself (the level-0 down-sweep). IIR_FUSED_MAXP=0 at build time
+// gives the unfused form (two more launches), kept for side-by-side measurement.
 #ifndef IIR_FUSED_MAXP
 #define IIR_FUSED_MAXP 8
 #endif

@@ -2,7 +2,7 @@
 # max abs error when evaluated in float32 (Lawson-weighted least squares toward minimax).
 import numpy as np
 # fit atan(t)/t = P(s), s = t^2, t in [0,1], weighted least squares on Chebyshev nodes, then check float32 eval
-for deg in (5, 6, 7):
+for deg in (4, 5, 6, 7):
     t = np.cos(np.pi * (np.arange(4000) + 0.5) / 4000) * 0.5 + 0.5
     s = t * t
     f = np.arctan(t) / np.where(t == 0, 1, t)

@@ -458,6 +458,11 @@ def secondary_configs(torch, ops, device, taps):
     out["qpsk256"]["modulate_awgn_us"] = round(ta * 1e6, 2)
     out["qpsk256"]["round_trip_us"] = round((ta + td) * 1e6, 2)
     out["qpsk256"]["round_trip_msymbols_per_s"] = round(n / (ta + td) / 1e6, 1)
+    # config 5's algorithmic bytes: 2^24 + 8 * 2^24 (modulate) + 8 * 2^24 + 2^24 (demodulate)
+    out["qpsk256"]["round_trip_frac_of_8tbps"] = round(18 * n / (ta + td) / 1e9 / HBM_PEAK_GBPS, 4)
+    for rec in out.values():  # every byte-rate figure also as a fraction of the 8 TB/s HBM peak
+        for k in [k for k in rec if k.startswith("alg_gbps")]:
+            rec[k.replace("alg_gbps", "frac_of_8tbps")] = round(rec[k] / HBM_PEAK_GBPS, 4)
     out["qpsk256"]["ser_awgn"] = round(float((rx_bytes != syms).float().mean()), 6)
     out["qpsk256"]["squared_distance_rule_disagreements"] = sq_rule_disagreements(torch, tx, 0)
     k5 = 1 << 20

@@ -219,33 +219,38 @@ hipError_t launch_d4_complex(const FirJob& j, hipStream_t s) {
   }
 }
 
-// Multi-channel chain (k_fir_multi): one launch per group of <= kMaxMultiChannels channels. Returns
-// hipErrorNotSupported when the shape does not apply (the caller then runs the channels one by one).
+// Multi-channel chain (k_fir_poly_grouped): one launch per group of <= kMaxMultiChannels channels, the
+// single-channel polyphase tile with the C channels of an input tile grouped on one XCD (same staging
+// choice as launch_poly, so each channel is that kernel's call bit for bit). Returns
+// hipErrorNotSupported, before launching anything, when the shape does not apply (the caller then runs
+// the channels one by one).
 template <class TapT, class InT, int D, int R, int JC, int WG, int MODE>
-hipError_t launch_multi(const FirJob& j, const MultiParams& mp, hipStream_t s) {
+hipError_t launch_multi_grouped(const FirJob& j, const MultiParams& mp, hipStream_t s) {
   using Geo = TileGeo<InT, D, R, WG>;
-  constexpr int HMAX = 1;
-  constexpr int BPT = Geo::SG * (Geo::KT / Geo::ROUT) / WG;
   FirParams p = make_params(j);
   const uint64_t rows = ceil_div<uint64_t>(j.T, (uint64_t)D);
   const uint64_t nch = ceil_div<uint64_t>(rows, (uint64_t)JC);
   const uint64_t span = nch * JC * D;
   if (span > 0x40000000ull) return hipErrorNotSupported;
-  const uint64_t NG = ((uint64_t)(Geo::KT - 1) * D + span + Geo::G - 1) / Geo::G;
-  if (NG > (uint64_t)(BPT + HMAX) * WG) return hipErrorNotSupported;  // halo does not fit the registers
   const size_t lds = poly_lds_bytes<InT, D, R, WG>((uint32_t)span, MODE);
   if (lds > kMaxTileLds) return hipErrorNotSupported;
   p.nch = (uint32_t)nch;
   const uint32_t stride = (MODE == kModeFm) ? fm_tile_stride<InT>(Geo::KT, j.D) : Geo::KT;
   p.tile_stride = stride;
   const uint64_t tiles = ceil_div<uint64_t>(j.N, stride);
-  if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
+  const uint64_t blocks = ceil_div<uint64_t>(tiles, 8) * 8 * mp.count;
+  if (blocks > 0x7fffffffull) return hipErrorNotSupported;
   constexpr uint64_t A = SampleT<InT>::kSrcAlign;
   const bool vec = (reinterpret_cast<uintptr_t>(j.in) % A) == 0 && ((uint64_t)stride * D * sizeof(InT)) % A == 0;
   if (vec) {
-    k_fir_multi<TapT, InT, D, R, JC, WG, HMAX, true, MODE, true><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p, mp);
+    k_fir_poly_grouped<TapT, InT, D, R, JC, WG, true, MODE><<<dim3((uint32_t)blocks), dim3(WG), lds, s>>>(
+        p, mp, (uint32_t)tiles);
+  } else if (shifted_staging<InT>(j.in, (uint64_t)stride * D)) {
+    k_fir_poly_grouped<TapT, InT, D, R, JC, WG, false, MODE, true><<<dim3((uint32_t)blocks), dim3(WG), lds, s>>>(
+        p, mp, (uint32_t)tiles);
   } else {
-    k_fir_multi<TapT, InT, D, R, JC, WG, HMAX, false, MODE, true><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p, mp);
+    k_fir_poly_grouped<TapT, InT, D, R, JC, WG, false, MODE><<<dim3((uint32_t)blocks), dim3(WG), lds, s>>>(
+        p, mp, (uint32_t)tiles);
   }
   return launch_status();
 }
@@ -256,11 +261,11 @@ hipError_t launch_multi_chain(const FirJob& j, const MultiParams& mp, hipStream_
   if (j.T > (1u << 26)) return hipErrorNotSupported;
   switch (j.D) {
     case 2:
-      return launch_multi<float, InT, 2, 8, 16, 128, MODE>(j, mp, s);
+      return launch_multi_grouped<float, InT, 2, 8, 16, 128, MODE>(j, mp, s);
     case 4:
-      return launch_multi<float, InT, 4, 4, 16, 256, MODE>(j, mp, s);
+      return launch_multi_grouped<float, InT, 4, 4, 16, 256, MODE>(j, mp, s);
     case 8:
-      return launch_multi<float, InT, 8, 2, 8, 256, MODE>(j, mp, s);
+      return launch_multi_grouped<float, InT, 8, 2, 8, 256, MODE>(j, mp, s);
     default:
       return hipErrorNotSupported;
   }

@@ -896,9 +896,10 @@ __device__ __forceinline__ uint32_t tile_of_block() {
   }
 }
 
-template <class TapT, class InT, int D, int R, int JC, int WG, bool VEC, int MODE, int ABL = 0, bool NT = false,
-          bool XM = false, int CST = 0, bool DMA = false, bool SH = false>
-__global__ __launch_bounds__(WG) void k_fir_poly(FirParams p) {
+// One tile of the polyphase kernel (the body of k_fir_poly and of k_fir_poly_grouped).
+template <class TapT, class InT, int D, int R, int JC, int WG, bool VEC, int MODE, int ABL, bool NT, int CST, bool DMA,
+          bool SH>
+__device__ __forceinline__ void fir_poly_tile(const FirParams& p, uint32_t tile) {
   using Geo = TileGeo<InT, D, R, WG>;
   using OutT = typename Product<TapT, InT>::type;
   constexpr int G = Geo::G;
@@ -906,7 +907,7 @@ __global__ __launch_bounds__(WG) void k_fir_poly(FirParams p) {
   extern __shared__ __attribute__((aligned(16))) float4 lds[];
   const InT* __restrict__ in = reinterpret_cast<const InT*>(p.in);
 
-  const uint64_t out0 = (uint64_t)tile_of_block<XM>() * p.tile_stride;
+  const uint64_t out0 = (uint64_t)tile * p.tile_stride;
   const uint64_t S0 = out0 * D;
   const uint32_t span = p.nch * JC * D;
   const uint32_t NG = ((Geo::KT - 1) * D + span + G - 1) / G;
@@ -945,13 +946,15 @@ __global__ __launch_bounds__(WG) void k_fir_poly(FirParams p) {
   tile_epilogue<MODE, OutT, R, WG, NT, true>(p, out0, acc, xs, lds);
 }
 
+template <class TapT, class InT, int D, int R, int JC, int WG, bool VEC, int MODE, int ABL = 0, bool NT = false,
+          bool XM = false, int CST = 0, bool DMA = false, bool SH = false>
+__global__ __launch_bounds__(WG) void k_fir_poly(FirParams p) {
+  fir_poly_tile<TapT, InT, D, R, JC, WG, VEC, MODE, ABL, NT, CST, DMA, SH>(p, tile_of_block<XM>());
+}
+
 // ------------------------------------------------------------------------------------------------
-// Kernel 1m: multi-channel NCO + FIR + demodulator (the intent of the
-// reference's dead k_Fm4x, src/fm.cu:71-179). The workgroup loads its input tile from HBM into
-// registers ONCE, then for each channel mixes it with that channel's NCO into the LDS tile, runs the
-// polyphase core and writes the channel's demodulated outputs. HBM input traffic is paid once for
-// all channels; the per-output arithmetic (NCO phasor, MAC order, epilogue) is the single-channel
-// kernel's, so channel c is bit-identical to gsdrFmDemod / gsdrAmDemod with its own frequency.
+// Multi-channel NCO + FIR + demodulator (the intent of the reference's
+// dead k_Fm4x, src/fm.cu:71-179): up to kMaxMultiChannels channels of one input per launch.
 // ------------------------------------------------------------------------------------------------
 constexpr int kMaxMultiChannels = 16;
 
@@ -961,80 +964,25 @@ struct MultiParams {
   float gain[kMaxMultiChannels];      // FM gain per channel
 };
 
-template <class TapT, class InT, int D, int R, int JC, int WG, int HMAX, bool VEC, int MODE, bool NT>
-__global__ __launch_bounds__(WG) void k_fir_multi(FirParams p, MultiParams mp) {
-  using Geo = TileGeo<InT, D, R, WG>;
-  using OutT = typename Product<TapT, InT>::type;
-  constexpr int G = Geo::G;
-  constexpr int BPT = Geo::SG * (Geo::KT / Geo::ROUT) / WG;
-  static_assert(MODE != kModeFir, "channels differ by their NCO");
-
-  extern __shared__ __attribute__((aligned(16))) float4 lds[];
-  const InT* __restrict__ in = reinterpret_cast<const InT*>(p.in);
-  const uint64_t out0 = (uint64_t)blockIdx.x * p.tile_stride;
-  const uint64_t S0 = out0 * D;
-  const uint32_t span = p.nch * JC * D;
-  const uint32_t NG = ((Geo::KT - 1) * D + span + G - 1) / G;
-  const uint32_t tid = threadIdx.x;
-
-  // the raw tile, held in registers across the channel loop (loaded as stage_tile does)
-  float4 body[BPT];
-  float4 halo[HMAX];
-  const bool whole = VEC && (S0 + (uint64_t)NG * G <= p.L);
-  if (whole) {
-    if constexpr (std::is_same<InT, Iq8>::value) {
-      const uint32_t* __restrict__ src = reinterpret_cast<const uint32_t*>(in + S0);
-#pragma unroll
-      for (int k = 0; k < BPT; ++k) body[k] = iq8x2_granule(NT ? __builtin_nontemporal_load(src + k * WG + tid) : src[k * WG + tid]);
-    } else {
-      const float4* __restrict__ src = reinterpret_cast<const float4*>(in + S0);
-#pragma unroll
-      for (int k = 0; k < BPT; ++k) body[k] = NT ? load16_nt(src + k * WG + tid) : src[k * WG + tid];
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < BPT; ++k) body[k] = load_granule<InT, VEC>(in, S0 + (uint64_t)(k * WG + tid) * G, p.L);
-  }
-#pragma unroll
-  for (int k = 0; k < HMAX; ++k) {
-    const uint32_t g = BPT * WG + k * WG + tid;
-    halo[k] = g < NG ? load_granule<InT, VEC>(in, S0 + (uint64_t)g * G, p.L) : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-
-  float2* xs = reinterpret_cast<float2*>(lds + Geo::padded(NG - 1) + 1);
-  for (uint32_t c = 0; c < mp.count; ++c) {
-    FirParams pc = p;
-    pc.nco_inc = mp.inc[c];
-    pc.fm_gain = mp.gain[c];
-    pc.out = reinterpret_cast<float*>(p.out) + (uint64_t)c * p.N;
-    const PhaseWalk pw = phase_walk<G, WG>(p.nco_n0, S0, pc.nco_inc);
-    auto mix = [&](auto odd_c) {  // one instantiation per (tile-uniform) NCO start parity, as stage_tile
-#pragma unroll
-      for (int k = 0; k < BPT; ++k) {
-        const uint32_t g = k * WG + tid;
-        lds[Geo::padded(g)] =
-            stage_transform_ph<InT, MODE>(body[k], pw.ph0 + (uint32_t)k * pw.step, decltype(odd_c)::value, pw.inc);
-      }
-    };
-    if (pw.odd) {
-      mix(std::true_type{});
-    } else {
-      mix(std::false_type{});
-    }
-#pragma unroll
-    for (int k = 0; k < HMAX; ++k) {
-      const uint32_t g = BPT * WG + k * WG + tid;
-      if (g < NG) lds[Geo::padded(g)] = stage_transform<InT, MODE>(halo[k], (uint32_t)S0 + g * G, pc);
-    }
-    __syncthreads();
-    OutT acc[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) set_zero(acc[r]);
-    poly_compute<TapT, InT, D, R, JC, WG>(lds, pc, acc);
-    if (!all_finite(acc)) poly_fixup<TapT, InT, D, R, JC, WG>(lds, pc, acc);
-    tile_epilogue<MODE, OutT, R, WG>(pc, out0, acc, xs);
-    __syncthreads();  // the next channel overwrites the tile
-  }
+// Kernel 1g: multi-channel chains as C single-channel tiles per input tile, grouped for the L2. Block b
+// runs channel c of tile t, with b mod 8 = t mod 8 and the C channels of a tile consecutive among the
+// blocks of that residue: workgroups are dispatched round-robin over the 8 XCDs, so the C workgroups of a
+// tile run close together on ONE XCD and all but the first stage the tile from that XCD's L2 rather
+// than HBM. Each block is exactly the single-channel kernel's tile (same template, same code), so
+// channel c is bit-identical to gsdrFmDemod / gsdrAmDemod with its own frequency by construction, at
+// the single-channel kernel's register budget. (The first multi-channel kernel read each input tile
+// into registers once and looped over the channels: 228 VGPRs, 2 waves per SIMD, 5 % slower.)
+template <class TapT, class InT, int D, int R, int JC, int WG, bool VEC, int MODE, bool SH = false>
+__global__ __launch_bounds__(WG) void k_fir_poly_grouped(FirParams p, MultiParams mp, uint32_t tiles) {
+  const uint32_t C = mp.count;
+  const uint32_t b = blockIdx.x, r = b >> 3;
+  const uint32_t tile = (r / C) * 8u + (b & 7u), c = r % C;
+  if (tile >= tiles) return;  // the grid is rounded up to whole groups of 8 tiles
+  FirParams pc = p;
+  pc.nco_inc = mp.inc[c];
+  pc.fm_gain = mp.gain[c];
+  pc.out = reinterpret_cast<float*>(p.out) + (uint64_t)c * p.N;
+  fir_poly_tile<TapT, InT, D, R, JC, WG, VEC, MODE, 0, true, 0, false, SH>(pc, tile);
 }
 
 // ------------------------------------------------------------------------------------------------

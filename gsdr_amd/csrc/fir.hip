@@ -92,6 +92,30 @@ hipError_t launch_fc_probe(const FirJob& j, hipStream_t s) {
         default: return launch_poly<float, float2, 4, 4, 16, 256, kModeFm, 25, true>(c, s);
       }
     }
+    // FM chain (config 3 shape) tile-shape sweep: 130 default (R 4, JC 16, WG 256), 131 R 8 WG 128,
+    // 132 JC 8, 133 R 2, 134 WG 128, 135 R 8 JC 8 WG 128, 136 default with the XCD-aware tile order
+    case 130:
+    case 131:
+    case 132:
+    case 133:
+    case 134:
+    case 135:
+    case 136: {
+      FirJob c = j;
+      c.mode = kModeFm;
+      c.N = j.N - 1;
+      c.nco_inc = 429496730u;  // 0.1 fs
+      c.fm_gain = 7.957747f;   // fs / (2 pi 0.02 fs)
+      switch (j.variant) {
+        case 130: return launch_poly<float, float2, 4, 4, 16, 256, kModeFm, 0, true>(c, s);
+        case 131: return launch_poly<float, float2, 4, 8, 16, 128, kModeFm, 0, true>(c, s);
+        case 132: return launch_poly<float, float2, 4, 4, 8, 256, kModeFm, 0, true>(c, s);
+        case 133: return launch_poly<float, float2, 4, 2, 16, 256, kModeFm, 0, true>(c, s);
+        case 134: return launch_poly<float, float2, 4, 4, 16, 128, kModeFm, 0, true>(c, s);
+        case 135: return launch_poly<float, float2, 4, 8, 8, 128, kModeFm, 0, true>(c, s);
+        default: return launch_poly<float, float2, 4, 4, 16, 256, kModeFm, 0, true, true>(c, s);
+      }
+    }
     case 110:
     case 111:
       return launch_stream_probe(j, s, j.variant == 111);

@@ -122,6 +122,30 @@ __device__ __forceinline__ int nearest_level(float v, float scale) {
 // boundary) the 9 candidates are ranked by cuCabsf in ascending index order with strict '<', as the
 // reference's exhaustive loop does (no point outside the 3 x 3 can be that close). Returns 256 when the
 // symbol needs the exhaustive search (outside |re|,|im| <= 4|a|, or NaN).
+// The near-tie ranking of demod_rect_fast's 3 x 3 candidates by cuCabsf, in ascending index order with
+// strict '<' as the reference's loop. Out of line: it runs for a few symbols in a million, and inlined
+// into each of a thread's 16 unrolled symbols (nine divisions and square roots each) it made the
+// kernel ~60 KB of code.
+__device__ __noinline__ uint32_t demod_rect_tie(float dx0, float dx1, float dx2, float dy0, float dy1, float dy2,
+                                                int i0, int q0) {
+  const float dx[3] = {dx0, dx1, dx2}, dy[3] = {dy0, dy1, dy2};
+  float best = INFINITY;
+  uint32_t idx = 0;
+#pragma unroll
+  for (int di = 0; di < 3; ++di) {
+#pragma unroll
+    for (int dq = 0; dq < 3; ++dq) {
+      // out-of-grid neighbours (padded +inf levels) give an infinite difference and never win
+      const float d = ref_cabsf(dx[di], dy[dq]);
+      if (d < best) {
+        best = d;
+        idx = (uint32_t)((i0 - 1 + di) * 16 + (q0 - 1 + dq));
+      }
+    }
+  }
+  return idx;
+}
+
 __device__ __forceinline__ uint32_t demod_rect_fast(const float* __restrict__ lxp, const float* __restrict__ lyp, float2 r,
                                                     float lim, float scale) {
   if (!(fabsf(r.x) <= lim && fabsf(r.y) <= lim)) return 256u;
@@ -143,21 +167,7 @@ __device__ __forceinline__ uint32_t demod_rect_fast(const float* __restrict__ lx
   const int b = ey[0] == eym ? 0 : (ey[1] == eym ? 1 : 2);
   const float thr = tie_threshold(__fadd_rn(exm, eym));
   if (__fadd_rn(ex2, eym) > thr && __fadd_rn(exm, ey2) > thr) return (uint32_t)((i0 - 1 + a) * 16 + (q0 - 1 + b));
-  float best = INFINITY;
-  uint32_t idx = 0;
-#pragma unroll
-  for (int di = 0; di < 3; ++di) {
-#pragma unroll
-    for (int dq = 0; dq < 3; ++dq) {
-      // out-of-grid neighbours (padded +inf levels) give an infinite difference and never win
-      const float d = ref_cabsf(dx[di], dy[dq]);
-      if (d < best) {
-        best = d;
-        idx = (uint32_t)((i0 - 1 + di) * 16 + (q0 - 1 + dq));
-      }
-    }
-  }
-  return idx;
+  return demod_rect_tie(dx[0], dx[1], dx[2], dy[0], dy[1], dy[2], i0, q0);
 }
 
 __device__ __forceinline__ void load_table(float2* lds_tab, uint32_t type) {

@@ -24,6 +24,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <map>
+#include <vector>
 
 #include "awgn.hpp"
 #include "gsdr/gsdr_ext.h"
@@ -39,20 +41,25 @@ constexpr int kCSym = 16;  // symbols per thread
 __constant__ float2 c_qpsk256_tables[2][256];
 
 // Circular table: per-cell candidate lists over a kCellGrid^2 grid covering [-R, R)^2, built on the
-// host by gsdrQpsk256InitConstellation. List of cell c = idx[start[c] .. start[c+1]), ascending.
-// A point is listed for a cell when its distance to the cell is at most the smallest worst-case
-// distance of any table point over the cell (plus a margin for float rounding), so every point that
-// can win the argmin anywhere in the cell -- ties included -- is on the list, and the argmin over the
-// list in index order is the exhaustive one -- for the squared distance and, with the near-tie
-// re-ranking of the demodulation kernel, for the reference's cuCabsf rule. R == 0 disables the lookup.
+// host by gsdrQpsk256InitConstellation. A point is listed for a cell when its distance to the cell is
+// at most the smallest worst-case distance of any table point over the cell (plus a margin for float
+// rounding), so every point that can win the argmin anywhere in the cell -- ties included -- is on the
+// list, and the argmin over the list in index order is the exhaustive one -- for the squared distance
+// and, with the near-tie re-ranking of the demodulation kernel, for the reference's cuCabsf rule.
+// R == 0 disables the lookup.
+// One 16-bit word per cell: length (bits 12-15) and, for a one-point list, the point itself (bits
+// 0-11), else the offset of the list in `lists` (ascending indices). Neighbouring cells mostly share
+// their lists, which are stored once: the circular table at any amplitude has 2,863 one-point cells
+// and 6,353 longer lists of which 1,078 are distinct (3,293 bytes), so one cell lookup decides 87 % of
+// noisy symbols with a single LDS load and the whole structure is 22.5 KB of LDS.
 constexpr int kCellGrid = 96;
-constexpr int kMaxCellEntries = 19456;  // 18,764 used by the circular table (any amplitude); LDS < 40 KB
+constexpr int kCellListBytes = 4096;  // 12-bit offsets
 constexpr double kCellSpan = 1.3;  // grid half-width R = 1.3 * max |c|: noisy symbols stay on the grid
 struct alignas(16) CircCells {
   float R;
   float inv_cs;  // kCellGrid / (2 R)
-  uint16_t start[kCellGrid * kCellGrid + 1];
-  alignas(4) uint8_t idx[kMaxCellEntries];
+  uint16_t cell[kCellGrid * kCellGrid];
+  uint8_t lists[kCellListBytes];
 };
 __device__ CircCells g_circ_cells;
 
@@ -277,10 +284,10 @@ template <int TYPE>
 __global__ __launch_bounds__(kCBlock) void k_c256_demod(C256Streams st, uint32_t n) {
   __shared__ float2 tab[256];
   __shared__ float lxp[18], lyp[18];  // rectangular levels, padded with +inf (demod_rect_fast)
-  // the circular cell lists: an LDS image of g_circ_cells (start offsets and candidate indices)
+  // the circular cell lists: an LDS image of g_circ_cells (cell words and the distinct lists)
   __shared__ uint4 ccells[TYPE == 0 ? 1 : sizeof(CircCells) / 16];
-  const uint16_t* cstart = reinterpret_cast<const CircCells*>(ccells)->start;
-  const uint8_t* cidx = reinterpret_cast<const CircCells*>(ccells)->idx;
+  const uint16_t* cword = reinterpret_cast<const CircCells*>(ccells)->cell;
+  const uint8_t* clists = reinterpret_cast<const CircCells*>(ccells)->lists;
   // circular full tiles: the tile's decisions, and per wave the symbols whose search is not finished
   // after the first four candidates (see below)
   __shared__ uint16_t otile[TYPE == 0 ? 1 : kCBlock * kCSym / 2];
@@ -293,8 +300,8 @@ __global__ __launch_bounds__(kCBlock) void k_c256_demod(C256Streams st, uint32_t
     lyp[threadIdx.x] = (k < 0 || k > 15) ? INFINITY : tsrc[k].y;
   }
   if (TYPE != 0 && g_circ_cells.R > 0.0f) {  // the circular candidate lists, into LDS
-    // 16-byte copies, all issued before the first LDS store (~37 KB: ten loads a lane; the per-entry
-    // 2-byte copy loop it replaces waited on each load in turn and cost ~5 % of the kernel)
+    // 16-byte copies, all issued before the first LDS store (22.5 KB: six loads a lane; a per-entry
+    // 2-byte copy loop waited on each load in turn and cost ~5 % of the kernel)
     constexpr uint32_t kWords = sizeof(CircCells) / 16, kFull = kWords / kCBlock;
     const uint4* src = reinterpret_cast<const uint4*>(&g_circ_cells);
     uint4 w[kFull], wt = make_uint4(0u, 0u, 0u, 0u);
@@ -326,8 +333,9 @@ __global__ __launch_bounds__(kCBlock) void k_c256_demod(C256Streams st, uint32_t
     } else {
       const float fx = (r.x + cR) * inv_cs, fy = (r.y + cR) * inv_cs;
       if (cR > 0.0f && fx >= 0.0f && fy >= 0.0f && fx < (float)kCellGrid && fy < (float)kCellGrid) {
-        const int c = (int)fy * kCellGrid + (int)fx;
-        const uint32_t b = cstart[c], e = cstart[c + 1];
+        const uint32_t wc = cword[(int)fy * kCellGrid + (int)fx], len = wc >> 12;
+        if (len == 1u) return wc & 0xfffu;  // a one-point cell: no distance needed
+        const uint32_t b = wc & 0xfffu, e = b + len;
         float best = INFINITY, second = INFINITY;
         uint32_t idx = 0;
         // four candidates per step with independent LDS loads; slots past the list end repeat its
@@ -336,7 +344,7 @@ __global__ __launch_bounds__(kCBlock) void k_c256_demod(C256Streams st, uint32_t
           uint32_t k[4];
           float2 pt[4];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) k[j] = cidx[m + j < e ? m + j : e - 1];
+          for (int j = 0; j < 4; ++j) k[j] = clists[m + j < e ? m + j : e - 1];
 #pragma unroll
           for (int j = 0; j < 4; ++j) pt[j] = tab[k[j]];
 #pragma unroll
@@ -357,7 +365,7 @@ __global__ __launch_bounds__(kCBlock) void k_c256_demod(C256Streams st, uint32_t
         best = INFINITY;
         idx = 0;
         for (uint32_t m = b; m < e; ++m) {
-          const uint32_t k = cidx[m];
+          const uint32_t k = clists[m];
           const float d = ref_dist(r, tab[k]);
           if (d < best) {
             best = d;
@@ -374,10 +382,9 @@ __global__ __launch_bounds__(kCBlock) void k_c256_demod(C256Streams st, uint32_t
   auto circ_first = [&](float2 r, uint32_t& idx) -> bool {
     const float fx = (r.x + cR) * inv_cs, fy = (r.y + cR) * inv_cs;
     if (!(cR > 0.0f && fx >= 0.0f && fy >= 0.0f && fx < (float)kCellGrid && fy < (float)kCellGrid)) return false;
-    const int c = (int)fy * kCellGrid + (int)fx;
-    const uint32_t b = cstart[c], e = cstart[c + 1];
-    idx = cidx[b];
-    return e - b == 1u;
+    const uint32_t wc = cword[(int)fy * kCellGrid + (int)fx];
+    idx = wc & 0xffu;  // the point of a one-point cell; the low byte of an offset otherwise (overwritten)
+    return (wc >> 12) == 1u;
   };
   // grid-stride over 4096-symbol tiles, so the LDS tables are staged once per workgroup
   const uint32_t tiles = (uint32_t)((n + (uint64_t)kCBlock * kCSym - 1) / ((uint64_t)kCBlock * kCSym));
@@ -446,8 +453,8 @@ __global__ __launch_bounds__(kCBlock) void k_c256_demod(C256Streams st, uint32_t
   }
 }
 
-// circular demodulation workgroups per stream (grid-stride): 3 resident per CU x 256 CUs (52 KB LDS)
-constexpr uint32_t kCircBlocks = 768;
+// circular demodulation workgroups per stream (grid-stride): 4 resident per CU x 256 CUs (37 KB LDS)
+constexpr uint32_t kCircBlocks = 1024;
 
 static hipError_t c256_launch(bool modulate, const C256Streams& st, int nstreams, uint32_t n, uint32_t type,
                               int32_t device, hipStream_t stream) {
@@ -464,7 +471,7 @@ static hipError_t c256_launch(bool modulate, const C256Streams& st, int nstreams
     k_c256_mod<<<grid, dim3(kCBlock), 0, stream>>>(st, n, type);
   } else {
     // rectangular: one workgroup per tile; circular: one resident round of workgroups (cell lists,
-    // decision tile and wave queues take 52 KB of LDS, 3 workgroups per CU) striding over the tiles
+    // decision tile and wave queues take 37 KB of LDS, 4 workgroups per CU) striding over the tiles
     const dim3 dgrid(type == 0 ? blocks : std::min<uint32_t>(blocks, kCircBlocks), (uint32_t)nstreams);
     if (type == 0) {
       k_c256_demod<0><<<dgrid, dim3(kCBlock), 0, stream>>>(st, n);
@@ -519,6 +526,8 @@ static bool build_cells(const float2* t, CircCells* cc) {
   const double cs = 1.0 / (double)inv_cs;
   const double margin = 1e-4 * rmax;  // >> float rounding of positions and distances
   int n = 0;
+  std::map<std::vector<uint8_t>, int> seen;  // distinct lists -> offset
+  std::vector<uint8_t> list;
   for (int iy = 0; iy < kCellGrid; ++iy) {
     for (int ix = 0; ix < kCellGrid; ++ix) {
       const double x0 = -(double)R + ix * cs, x1 = x0 + cs, y0 = -(double)R + iy * cs, y1 = y0 + cs;
@@ -530,21 +539,28 @@ static bool build_cells(const float2* t, CircCells* cc) {
       }
       const double bound = std::sqrt(bound2) + margin;
       const double lim2 = bound * bound;
-      cc->start[iy * kCellGrid + ix] = (uint16_t)n;
+      list.clear();
       for (int p = 0; p < 256; ++p) {
         const double dx = std::max({x0 - t[p].x, 0.0, t[p].x - x1});
         const double dy = std::max({y0 - t[p].y, 0.0, t[p].y - y1});
-        if (dx * dx + dy * dy <= lim2) {
-          if (n >= kMaxCellEntries) {
-            cc->R = 0.0f;
-            return true;  // does not fit: keep the exhaustive search
-          }
-          cc->idx[n++] = (uint8_t)p;
-        }
+        if (dx * dx + dy * dy <= lim2) list.push_back((uint8_t)p);
       }
+      const int len = (int)list.size();  // >= 1: the point defining the bound is always listed
+      if (len < 1 || len > 15) return true;  // does not fit the cell word: keep the exhaustive search
+      int field = list[0];
+      if (len > 1) {
+        auto it = seen.find(list);
+        if (it == seen.end()) {
+          if (n + len > kCellListBytes) return true;  // does not fit: keep the exhaustive search
+          std::copy(list.begin(), list.end(), cc->lists + n);
+          it = seen.emplace(list, n).first;
+          n += len;
+        }
+        field = it->second;
+      }
+      cc->cell[iy * kCellGrid + ix] = (uint16_t)((len << 12) | field);
     }
   }
-  cc->start[kCellGrid * kCellGrid] = (uint16_t)n;
   cc->R = R;
   cc->inv_cs = inv_cs;
   return true;
@@ -566,7 +582,11 @@ GSDR_C_LINKAGE hipError_t gsdrQpsk256InitConstellation(uint32_t constellationTyp
   if (st != hipSuccess) return st;
   static thread_local gsdr::CircCells cells;  // host staging (~38 KiB): waited for below
   if (constellationType != 0) {
-    gsdr::build_cells(table, &cells);
+    try {
+      gsdr::build_cells(table, &cells);
+    } catch (...) {  // allocation failure: no lookup, the exhaustive search stays exact
+      cells.R = 0.0f;
+    }
     st = hipMemcpyToSymbolAsync(HIP_SYMBOL(gsdr::g_circ_cells), &cells, sizeof(cells), 0, hipMemcpyHostToDevice,
                                 cudaStream);
   }

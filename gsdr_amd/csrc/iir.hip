@@ -230,6 +230,11 @@ struct ScanArgs {
   const double* T0;      // M_0^r, r < 64 (final pass)
   const double* gstart;  // level-1 start states (final pass), or null: s0 is the group start
   const double* s0;
+  // level-1 down-sweep folded into the final pass (levels >= 2): the level-1 inclusive prefixes, M_1^r
+  // and the level-2 start states; then gstart is unused
+  const double* incl1;
+  const double* T1;
+  const double* gstart2;
 };
 
 // Up-sweep of one level-0 group from the workgroup's tails in LDS (loc = the group's 64 elements),
@@ -371,10 +376,28 @@ __global__ __launch_bounds__(TileShape<S>::WG) void k_iir_chunks(Coeffs cf, cons
         const uint64_t g = c / kGroup;
         const int r = (int)(c % kGroup);
         const double* __restrict__ Mr = sc.T0 + (size_t)r * P * P;
-        const double* __restrict__ sg = sc.gstart ? sc.gstart + g * P * NC : sc.s0;
         double sgc[P];
+        if (sc.incl1) {
+          // the group's start = level-1 element g's start, M_1^r1 S_(g / 64) + prefix1_(g - 1) (as
+          // down_group), in place of a level-1 down-sweep launch
+          const uint64_t g2 = g / kGroup;
+          const int r1 = (int)(g % kGroup);
+          const double* __restrict__ M1 = sc.T1 + (size_t)r1 * P * P;
+          double s2[P];
 #pragma unroll
-        for (int l = 0; l < P; ++l) sgc[l] = sg[l * NC + comp];
+          for (int l = 0; l < P; ++l) s2[l] = sc.gstart2[(g2 * P + l) * NC + comp];
+#pragma unroll
+          for (int i = 0; i < P; ++i) {
+            double acc = r1 > 0 ? sc.incl1[((g - 1) * P + i) * NC + comp] : 0.0;
+#pragma unroll
+            for (int l = 0; l < P; ++l) acc = fma(M1[i * P + l], s2[l], acc);
+            sgc[i] = acc;
+          }
+        } else {
+          const double* __restrict__ sg = sc.gstart ? sc.gstart + g * P * NC : sc.s0;
+#pragma unroll
+          for (int l = 0; l < P; ++l) sgc[l] = sg[l * NC + comp];
+        }
 #pragma unroll
         for (int i = 0; i < P; ++i) {
           double acc = r > 0 ? sc.incl[((c - 1) * P + i) * NC + comp] : 0.0;
@@ -694,18 +717,27 @@ static hipError_t run(const Coeffs& cf, S* xh, S* yh, const S* x, S* y, uint64_t
   const int lowest = F ? 1 : 0;  // levels scanned outside the chunk passes
   int rest = lowest;             // first level handled by the single-workgroup kernels
   while (rest <= levels && ceil_div<uint64_t>(E[rest], kGroup) > (uint64_t)kRestGroups) ++rest;
+  // With the level-0 scan fused, the final pass also takes level 1's down-sweep (levels >= 2, level 1
+  // scanned by its own up-sweep launch): 2^24 samples in 4 launches (tails, level-1 up, levels 2-3,
+  // final) instead of 5.
+  const bool fold1 = F && levels >= 2 && rest >= 2;
   for (int k = lowest; k < rest; ++k) {
     k_iir_up<A, P><<<(uint32_t)ceil_div<uint64_t>(E[k], kGroup), 64, 0, st>>>(elems(k), E[k], table(k), starts(k),
                                                                              elems(k + 1));
   }
   if (rest <= levels) k_iir_scan_rest<A, P><<<1, 64 * kRestWaves, 0, st>>>(L, s0, rest);
-  for (int k = rest - 1; k >= lowest; --k) {
+  for (int k = rest - 1; k >= (fold1 ? 2 : lowest); --k) {
     k_iir_down<A, P><<<(uint32_t)ceil_div<uint64_t>(E[k], kGroup), 64, 0, st>>>(E[k], table(k), starts(k + 1),
                                                                                starts(k));
   }
-  const ScanArgs down_args{reinterpret_cast<double*>(starts(0)), nullptr, table(0),
+  const ScanArgs down_args{reinterpret_cast<double*>(starts(0)),
+                           nullptr,
+                           table(0),
                            levels > 0 ? reinterpret_cast<const double*>(starts(1)) : nullptr,
-                           reinterpret_cast<const double*>(s0)};
+                           reinterpret_cast<const double*>(s0),
+                           fold1 ? reinterpret_cast<const double*>(starts(1)) : nullptr,
+                           fold1 ? table(1) : nullptr,
+                           fold1 ? reinterpret_cast<const double*>(starts(2)) : nullptr};
   if (vec) {
     k_iir_chunks<S, P, kFinal, true, F><<<blocks, WG, 0, st>>>(cf, x, xh, n, starts(0), st_out, y, SetupArgs{},
                                                                down_args);

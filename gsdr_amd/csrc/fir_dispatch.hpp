@@ -19,6 +19,7 @@
 #include <type_traits>
 
 #include "fir_engine.hpp"
+#include "fir_i8_mfma.hpp"
 #include "launch.hpp"
 
 namespace gsdr {
@@ -271,6 +272,31 @@ hipError_t launch_multi_chain(const FirJob& j, const MultiParams& mp, hipStream_
   }
 }
 
+// int8 I/Q FIR on the matrix cores (k_fir_i8_mfma, fir_i8_mfma.hpp): D = 4, T <= I8Mfma<4>::MAXT,
+// 16-byte aligned output; persistent workgroups (their tap fragments are built once).
+template <int D, int BPC = 4>
+hipError_t launch_i8_mfma(const FirJob& j, hipStream_t s) {
+  using C = I8Mfma<D>;
+  if (j.D != (size_t)D || j.T < 1 || j.T > (size_t)C::MAXT || (reinterpret_cast<uintptr_t>(j.out) % 16) != 0) {
+    return hipErrorInvalidValue;
+  }
+  FirParams p = make_params(j);
+  const uint32_t ns = (uint32_t)ceil_div<uint64_t>(15u * D + j.T, 32u);
+  const uint64_t tiles = ceil_div<uint64_t>(j.N, (uint64_t)C::KT);
+  if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
+  int dev = 0, cus = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e != hipSuccess) return e;
+  const uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)cus * BPC);
+  if ((reinterpret_cast<uintptr_t>(j.in) % 16) == 0) {
+    k_fir_i8_mfma<D, true, BPC><<<dim3(grid), dim3(C::WG), 0, s>>>(p, ns, (uint32_t)tiles);
+  } else {
+    k_fir_i8_mfma<D, false, BPC><<<dim3(grid), dim3(C::WG), 0, s>>>(p, ns, (uint32_t)tiles);
+  }
+  return launch_status();
+}
+
 // tile-shape sweep for the int8 front end (gsdrxFirFCInt8Variant): the shapes of launch_d4_complex
 // whose staging is generic over the input type
 inline hipError_t launch_d4_int8(const FirJob& j, hipStream_t s) {
@@ -291,6 +317,10 @@ inline hipError_t launch_d4_int8(const FirJob& j, hipStream_t s) {
       return launch_poly<float, Iq8, 4, 4, 16, 64, kModeFir, 0, true>(j, s);
     case 28:
       return launch_poly<float, Iq8, 4, 4, 16, 128, kModeFir, 0, true>(j, s);
+    case 40:  // matrix cores (fp16 products, normwise parity), 4 workgroups per CU (128 VGPRs, spills)
+      return launch_i8_mfma<4, 4>(j, s);
+    case 41:  // matrix cores, 3 workgroups per CU: the default for D = 4
+      return launch_i8_mfma<4, 3>(j, s);
     default:
       return hipErrorInvalidValue;
   }
@@ -423,7 +453,15 @@ hipError_t launch_fir(const FirJob& j, hipStream_t s) {
     if constexpr (MODE == kModeFir) {
       if (j.D == 4 && j.variant >= 0) return launch_d4_int8(j, s);
     }
-    // the float-input shapes, so int8 and float inputs of one decimation give bit-identical outputs
+    // D = 4 FIR: the matrix-core kernel (fp16-exact samples, two-part taps; normwise parity with the
+    // float path, twice its speed: DESIGN.md section 3.3)
+    if constexpr (MODE == kModeFir && std::is_same<TapT, float>::value) {
+      if (j.D == 4 && j.T <= (size_t)I8Mfma<4>::MAXT && (reinterpret_cast<uintptr_t>(j.out) % 16) == 0) {
+        return launch_i8_mfma<4, 3>(j, s);
+      }
+    }
+    // otherwise the float-input shapes, so int8 and float inputs of one decimation give bit-identical
+    // outputs
     switch (j.D) {
       case 1:
         return launch_contig<TapT, InT, 1, 8, 16, 256, MODE>(j, s);

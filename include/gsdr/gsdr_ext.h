@@ -58,7 +58,15 @@ GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxFirFCVariant(
  * arguments -- without the float intermediate in HBM (2 instead of 8 input bytes per sample).
  */
 
-/** gsdrFirFC (fir.h) on int8 I/Q input. */
+/**
+ * gsdrFirFC (fir.h) on int8 I/Q input.
+ * Exception to the bit-identity above: decimation 4 with tapCount <= 196 and a 16-byte aligned output
+ * runs on the matrix cores (samples exact in fp16, taps scaled by a power of two and split into two
+ * fp16 parts, fp32 accumulation in the matrix core's order), which meets the floating-point parity bar
+ * of the float path -- max_k |y - y_float| / sum_i |t_i||x_(4k+i)| <= 1e-5 -- rather than matching it
+ * bit for bit; taps that are not all finite take the exact ascending loop. Variant 0 of
+ * gsdrxFirFCInt8Variant is the bit-identical packed-VALU path.
+ */
 GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxFirFCInt8(
     size_t decimation,
     const float* taps,
@@ -69,7 +77,8 @@ GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxFirFCInt8(
     int32_t cudaDevice,
     hipStream_t cudaStream) GSDR_NO_EXCEPT;
 
-/** gsdrxFirFCInt8 with an explicit decimation-4 tile shape (tuning sweep; -1 = default). */
+/** gsdrxFirFCInt8 with an explicit decimation-4 tile shape (tuning sweep; -1 = default; 40 / 41 = the
+ *  matrix-core kernel at 4 / 3 workgroups per CU). */
 GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxFirFCInt8Variant(
     int variant,
     size_t decimation,

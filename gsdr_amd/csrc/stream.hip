@@ -67,8 +67,11 @@ hipError_t filter(const gsdrxStream_t& s, const void* in, uint64_t first, void* 
   const bool i8 = s.format == GSDRX_SAMPLES_CS8;
   switch (s.kind) {
     case GSDRX_STREAM_FIR:
-      return i8 ? gsdrxFirFCInt8(s.D, s.taps, s.T, static_cast<const int8_t*>(in), static_cast<hipFloatComplex*>(out),
-                                 n, s.device, st)
+      // variant 0: the exact packed-VALU path for every decimation. The matrix-core default of
+      // gsdrxFirFCInt8 (D = 4) sums in an order that depends on an output's position within its 16-output
+      // block, i.e. on where a call starts, so chunked calls could not reproduce one monolithic call.
+      return i8 ? gsdrxFirFCInt8Variant(0, s.D, s.taps, s.T, static_cast<const int8_t*>(in),
+                                        static_cast<hipFloatComplex*>(out), n, s.device, st)
                 : gsdrFirFC(s.D, s.taps, s.T, static_cast<const hipFloatComplex*>(in),
                             static_cast<hipFloatComplex*>(out), n, s.device, st);
     case GSDRX_STREAM_FM:

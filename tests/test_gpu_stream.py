@@ -24,7 +24,9 @@ def monolithic(kind, x, taps, D, n0, int8):
     from gsdr_amd import ops
 
     if kind == "fir":
-        return ops.fir(taps, x, D)
+        # int8: the exact path (variant 0) the stream object runs; the D = 4 matrix-core default sums in
+        # a position-dependent order (stream.h)
+        return ops.fir_variant(0, taps, x, D) if int8 else ops.fir(taps, x, D)
     if kind == "fm":
         return ops.fm_demod(x, taps, FS, TUNE, CHAN, DEV, D, n0)
     return ops.am_demod(x, taps, FS, TUNE, CHAN, D, n0)

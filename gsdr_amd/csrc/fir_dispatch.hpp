@@ -20,7 +20,6 @@
 
 #include "fir_engine.hpp"
 #include "fir_i8_mfma.hpp"
-#include "fir_f32_mfma.hpp"
 #include "launch.hpp"
 
 namespace gsdr {
@@ -168,30 +167,6 @@ hipError_t launch_contig(const FirJob& j, hipStream_t s) {
   return launch_status();
 }
 
-// complex<float> FIR on the matrix cores (k_fir_f32_mfma): D = 4, T <= 132, 16-byte aligned output
-template <int NCT, int BPC, bool NOFIX = false>
-hipError_t launch_f32_mfma(const FirJob& j, hipStream_t s) {
-  using C = F32Mfma<NCT>;
-  if (j.D != 4 || j.T < 1 || j.T > (size_t)C::MAXT || (reinterpret_cast<uintptr_t>(j.out) % 16) != 0) {
-    return hipErrorInvalidValue;
-  }
-  FirParams p = make_params(j);
-  const uint32_t ns = (uint32_t)ceil_div<uint64_t>(15u * 4u + j.T, 32u);
-  const uint64_t tiles = ceil_div<uint64_t>(j.N, (uint64_t)C::KT);
-  if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
-  int dev = 0, cus = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  if (e != hipSuccess) return e;
-  const uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)cus * BPC);
-  if ((reinterpret_cast<uintptr_t>(j.in) % 16) == 0) {
-    k_fir_f32_mfma<NCT, true, BPC, NOFIX><<<dim3(grid), dim3(C::WG), 0, s>>>(p, ns, (uint32_t)tiles);
-  } else {
-    k_fir_f32_mfma<NCT, false, BPC, NOFIX><<<dim3(grid), dim3(C::WG), 0, s>>>(p, ns, (uint32_t)tiles);
-  }
-  return launch_status();
-}
-
 // Tile-shape variants of the headline case (real taps, complex input, D = 4), selectable through
 // gsdrxFirFCVariant for tuning sweeps (all with non-temporal streaming unless noted):
 //   0 default WG=256 R=4 JC=16 | 1 WG=128 R=8 | 3 WG=64 R=8 | 4 WG=128 R=8 JC=32 | 5 WG=256 R=4 JC=8
@@ -236,17 +211,6 @@ hipError_t launch_d4_complex(const FirJob& j, hipStream_t s) {
       return hipErrorInvalidValue;
     case 14:  // default shape, tile body staged by LDS-DMA (global_load_lds), non-temporal
       return launch_poly<TapT, InT, 4, 4, 16, 256, MODE, 0, true, false, 0, true>(j, s);
-    case 42:  // matrix cores, two-part fp16 split per 32-sample chunk (k_fir_f32_mfma), 3 workgroups / CU
-    case 43:  // the same, 2 workgroups / CU
-    case 44:  // 512 outputs a wave and tile, 2 workgroups / CU
-    case 45:
-      if constexpr (MODE == kModeFir && std::is_same<TapT, float>::value && std::is_same<InT, float2>::value) {
-        if (j.variant == 42) return launch_f32_mfma<2, 3>(j, s);
-        if (j.variant == 43) return launch_f32_mfma<2, 2>(j, s);
-        if (j.variant == 45) return launch_f32_mfma<2, 3, true>(j, s);  // timing probe: no chunk checks
-        return launch_f32_mfma<4, 2>(j, s);
-      }
-      return hipErrorInvalidValue;
     case 24:
       return launch_poly<TapT, InT, 4, 4, 16, 64, MODE, 0, true>(j, s);
     case 28:

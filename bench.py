@@ -394,7 +394,7 @@ def secondary_configs(torch, ops, device, taps):
         xi = torch.rand(n, dtype=dt, device=device, generator=g)
         yi = torch.empty_like(xi)
         argsets = [(bb.data_ptr(), aa.data_ptr(), 5, None, None, xi.data_ptr(), yi.data_ptr(), n, device.index, stream)]
-        t = time_abi(torch, getattr(abi.lib, name), argsets, reps=20, settle=100)
+        t = time_abi(torch, getattr(abi.lib, name), argsets, reps=100, settle=200)
         out[f"iir_{'cc' if dt == torch.complex64 else 'ff'}"] = {
             "config": f"{name}, 4th-order Butterworth (K = 5), 2^24 samples, parallel scan",
             "us_per_launch": round(t * 1e6, 2), "msamples_per_s": round(n / t / 1e6, 1),

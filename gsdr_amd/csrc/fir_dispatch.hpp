@@ -297,6 +297,28 @@ hipError_t launch_i8_mfma(const FirJob& j, hipStream_t s) {
   return launch_status();
 }
 
+// int8 I/Q FM / AM chain on the matrix cores (k_chain_i8_mfma): D = 4, T <= 132 (AM: 8-byte aligned output)
+template <int MODE>
+hipError_t launch_chain_i8_mfma(const FirJob& j, hipStream_t s) {
+  using C = I8ChainMfma<MODE>;
+  constexpr int BPC = 2;
+  FirParams p = make_params(j);
+  const uint32_t ns = (uint32_t)ceil_div<uint64_t>(15u * 4u + j.T, 32u);
+  const uint64_t tiles = ceil_div<uint64_t>(j.N, (uint64_t)C::STRIDE);
+  if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
+  int dev = 0, cus = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e != hipSuccess) return e;
+  const uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)cus * BPC);
+  if ((reinterpret_cast<uintptr_t>(j.in) % 8) == 0) {
+    k_chain_i8_mfma<MODE, true, BPC><<<dim3(grid), dim3(C::WG), 0, s>>>(p, ns, (uint32_t)tiles);
+  } else {
+    k_chain_i8_mfma<MODE, false, BPC><<<dim3(grid), dim3(C::WG), 0, s>>>(p, ns, (uint32_t)tiles);
+  }
+  return launch_status();
+}
+
 // tile-shape sweep for the int8 front end (gsdrxFirFCInt8Variant): the shapes of launch_d4_complex
 // whose staging is generic over the input type
 inline hipError_t launch_d4_int8(const FirJob& j, hipStream_t s) {
@@ -452,6 +474,14 @@ hipError_t launch_fir(const FirJob& j, hipStream_t s) {
     // int8 I/Q
     if constexpr (MODE == kModeFir) {
       if (j.D == 4 && j.variant >= 0) return launch_d4_int8(j, s);
+    }
+    // D = 4 FM / AM chains: the matrix-core kernel with the NCO folded into complex taps (normwise
+    // parity with the float chains: DESIGN.md section 3.3); variant 0 keeps the exact path (streams)
+    if constexpr (MODE != kModeFir && std::is_same<TapT, float>::value) {
+      if (j.D == 4 && j.variant < 0 && j.T <= (size_t)I8ChainMfma<MODE>::MAXT &&
+          (MODE == kModeFm || (reinterpret_cast<uintptr_t>(j.out) % 8) == 0)) {
+        return launch_chain_i8_mfma<MODE>(j, s);
+      }
     }
     // D = 4 FIR: the matrix-core kernel (fp16-exact samples, two-part taps; normwise parity with the
     // float path, twice its speed: DESIGN.md section 3.3)

@@ -191,4 +191,228 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
   }
 }
 
+
+
+// ------------------------------------------------------------------------------------------------
+// int8 I/Q FM / AM chains on the matrix cores (gsdrxFmDemodInt8 / gsdrxAmDemodInt8, D = 4, T <= 132).
+// The NCO moves into the taps: with phi(n) the mixer phase of sample n (exact integer phase, fir_engine.hpp),
+//   y[k] = sum_i t_i x[4k+i] e^{j phi(4k+i)} = e^{j phi(4k)} y'[k],  y'[k] = sum_i t'_i x[4k+i],
+//   t'_i = t_i e^{j 2 pi (i inc mod 2^32) / 2^32}
+// (the phase is additive mod 2^32). The AM envelope |y| = |y'|, and the FM discriminator
+// arg(y[k+1] conj y[k]) = arg(y'[k+1] conj y'[k]) + 2 pi (4 inc mod 2^32) / 2^32 (wrapped), so neither
+// needs the rotation: the chain is a complex-tap FIR on the raw int8 samples, exact in fp16 as in
+// k_fir_i8_mfma. Complex taps on real planes: with P/Q' the real/imaginary-tap sums of the I column and
+// R/S those of the Q column, y' = (P - S) + j (R + Q'); two fp16 parts per tap component -> 4 MFMAs per
+// 32-sample step. FM tiles overlap by one output (stride KT - 1) and stage 8-byte granules, so every
+// tile start stays aligned. Normwise parity with the float chains, not bit identity (gsdr_ext.h).
+// ------------------------------------------------------------------------------------------------
+template <int MODE>
+struct I8ChainMfma {
+  static constexpr int D = 4;
+  static constexpr int WG = 256;
+  static constexpr int NCT = 4;
+  static constexpr int KT = (WG / 64) * NCT * 128;
+  static constexpr int STRIDE = MODE == kModeFm ? KT - 1 : KT;
+  static constexpr int MAXNS = 6;
+  static constexpr int MAXT = 32 * MAXNS - 15 * D;  // 132
+  static constexpr int SPAN = (KT - 16) * D + 32 * MAXNS;
+  static constexpr int NG = SPAN / 4;  // 8-byte granules (4 samples)
+  static constexpr int NGR = (NG + WG - 1) / WG;
+  static_assert(SPAN % 4 == 0, "whole granules");
+  __host__ __device__ static constexpr uint32_t addr(uint32_t idx) { return idx * 2u + (idx / 64u) * 16u; }
+  static constexpr uint32_t PLANE = (addr(SPAN) + 255u) / 256u * 256u + 128u;
+  static constexpr uint32_t LDS_BYTES = PLANE + addr(SPAN);
+  static_assert(LDS_BYTES >= (uint32_t)KT * 8u, "the FM output pass reuses the planes");
+};
+
+template <int MODE, bool VEC, int BPC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC))) void k_chain_i8_mfma(FirParams p, uint32_t ns, uint32_t tiles) {
+  using C = I8ChainMfma<MODE>;
+  constexpr int D = C::D;
+  __shared__ __attribute__((aligned(16))) char lds[C::LDS_BYTES];
+  __shared__ float wmax[C::WG / 64];
+  __shared__ uint32_t wbad[C::WG / 64];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+  const float* __restrict__ taps = reinterpret_cast<const float*>(p.taps);
+  const Iq8* __restrict__ in = reinterpret_cast<const Iq8*>(p.in);
+  float* __restrict__ out = reinterpret_cast<float*>(p.out);
+  const uint32_t T = p.T;
+
+  // modulated taps t'_i = t_i e^{j 2 pi (i inc) / 2^32}
+  const float t = tid < T ? taps[tid] : 0.0f;
+  const float2 ph = nco_direct(tid * p.nco_inc);
+  const float tr = t * ph.x, ti = t * ph.y;
+  float a = fmaxf(fabsf(tr), fabsf(ti));
+  uint32_t bad = isfinite(t) ? 0u : 1u;
+  for (int o = 32; o > 0; o >>= 1) {
+    a = fmaxf(a, __shfl_xor(a, o, 64));
+    bad |= __shfl_xor(bad, o, 64);
+  }
+  if (lane == 0) {
+    wmax[w] = a;
+    wbad[w] = bad;
+  }
+  __syncthreads();
+  float amax = wmax[0];
+  bad = wbad[0];
+#pragma unroll
+  for (int i = 1; i < C::WG / 64; ++i) {
+    amax = fmaxf(amax, wmax[i]);
+    bad |= wbad[i];
+  }
+  if (bad) {  // non-finite taps: the exact per-output chain (the generic kernel's evaluation)
+    for (uint32_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+      for (uint32_t r = tid; r < (uint32_t)C::STRIDE; r += C::WG) {
+        const uint64_t k = (uint64_t)tile * C::STRIDE + r;
+        if (k >= p.N) continue;
+        const float2 y0 = fir_point<float, Iq8, MODE>(p, k);
+        if constexpr (MODE == kModeFm) {
+          out[k] = fm_disc(y0, fir_point<float, Iq8, MODE>(p, k + 1), p.fm_gain);
+        } else {
+          out[k] = am_env(y0);
+        }
+      }
+    }
+    return;
+  }
+  int e = 0;
+  (void)frexpf(amax, &e);
+  const int sc = 14 - e;
+  float* ldsT = reinterpret_cast<float*>(lds);
+  ldsT[tid] = ldexpf(tr, sc);
+  ldsT[C::WG + tid] = ldexpf(ti, sc);
+  __syncthreads();
+  gsdr_h8 arh[C::MAXNS], arl[C::MAXNS], aih[C::MAXNS], ail[C::MAXNS];
+  {
+    const int m = (int)(lane & 15u), q = (int)(lane >> 4);
+#pragma unroll
+    for (int s = 0; s < C::MAXNS; ++s) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = 32 * s + 8 * q + j - D * m;  // <= 191 < WG
+        const float vr = i >= 0 ? ldsT[i] : 0.0f, vi = i >= 0 ? ldsT[C::WG + i] : 0.0f;
+        const _Float16 hr = (_Float16)vr, hi = (_Float16)vi;
+        arh[s][j] = hr;
+        arl[s][j] = (_Float16)(vr - (float)hr);
+        aih[s][j] = hi;
+        ail[s][j] = (_Float16)(vi - (float)hi);
+      }
+    }
+  }
+  const float oscale = ldexpf(1.0f / 127.0f, -sc);
+  // FM: the rotation the taps leave out, 2 pi (4 inc mod 2^32) / 2^32 in (-pi, pi]
+  const float dphi = (float)((double)(int32_t)(4u * p.nco_inc) * (6.283185307179586 / 4294967296.0));
+  __syncthreads();
+
+  const int n = (int)(lane & 15u), q = (int)(lane >> 4), c = n & 1, b = n >> 1;
+  const char* bplane = lds + (c ? C::PLANE : 0u);
+  for (uint32_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+    const uint64_t k_t = (uint64_t)tile * C::STRIDE;
+    const uint64_t S0 = k_t * D;
+    uint2 wv[C::NGR];
+#pragma unroll
+    for (int r = 0; r < C::NGR; ++r) {
+      const uint32_t g = tid + (uint32_t)r * C::WG;
+      const uint64_t s = S0 + 4ull * g;
+      wv[r] = make_uint2(0u, 0u);
+      if (g < (uint32_t)C::NG) {
+        if (VEC && s + 4 <= p.L) {
+          typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+          const u2v t2 = __builtin_nontemporal_load(reinterpret_cast<const u2v*>(in + s));
+          wv[r] = make_uint2(t2.x, t2.y);
+        } else {
+          uint32_t d[2];
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            const Iq8 a0 = s + 2 * k < p.L ? in[s + 2 * k] : Iq8{0, 0};
+            const Iq8 a1 = s + 2 * k + 1 < p.L ? in[s + 2 * k + 1] : Iq8{0, 0};
+            d[k] = (uint32_t)(uint8_t)a0.x | (uint32_t)(uint8_t)a0.y << 8 | (uint32_t)(uint8_t)a1.x << 16 |
+                   (uint32_t)(uint8_t)a1.y << 24;
+          }
+          wv[r] = make_uint2(d[0], d[1]);
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < C::NGR; ++r) {
+      const uint32_t g = tid + (uint32_t)r * C::WG;
+      if (g < (uint32_t)C::NG) {
+        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+        h4 hi_, hq_;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const uint32_t wd = k ? wv[r].y : wv[r].x;
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {  // gsdrInt8ToNormFloat clamps -128 to -1.0 = -127 / 127
+            hi_[2 * k + u] = (_Float16)max((int)(wd << (24 - 16 * u)) >> 24, -127);
+            hq_[2 * k + u] = (_Float16)max((int)(wd << (16 - 16 * u)) >> 24, -127);
+          }
+        }
+        const uint32_t o = C::addr(4u * g);
+        *reinterpret_cast<h4*>(lds + o) = hi_;
+        *reinterpret_cast<h4*>(lds + C::PLANE + o) = hq_;
+      }
+    }
+    __syncthreads();
+    float4 res[C::NCT];
+#pragma unroll
+    for (int ct = 0; ct < C::NCT; ++ct) {
+      const uint32_t cbase = (w * C::NCT + (uint32_t)ct) * 128u;
+      const uint32_t idx0 = (cbase + 16u * (uint32_t)b) * D + 8u * (uint32_t)q;
+      gsdr_f4v ar = {0.0f, 0.0f, 0.0f, 0.0f}, ai = ar;
+#pragma unroll
+      for (int s = 0; s < C::MAXNS; ++s) {
+        if ((uint32_t)s < ns) {
+          const gsdr_h8 bf = *reinterpret_cast<const gsdr_h8*>(bplane + C::addr(idx0 + 32u * (uint32_t)s));
+          ar = __builtin_amdgcn_mfma_f32_16x16x32_f16(arl[s], bf, ar, 0, 0, 0);
+          ai = __builtin_amdgcn_mfma_f32_16x16x32_f16(ail[s], bf, ai, 0, 0, 0);
+          ar = __builtin_amdgcn_mfma_f32_16x16x32_f16(arh[s], bf, ar, 0, 0, 0);
+          ai = __builtin_amdgcn_mfma_f32_16x16x32_f16(aih[s], bf, ai, 0, 0, 0);
+        }
+      }
+      // I lane (c = 0): ar = P, ai = Q'; Q lane: ar = R, ai = S.  y' = (P - S) + j (R + Q')
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float other = __shfl_xor(ai[i], 1, 64);
+        v[i] = (c ? ar[i] + other : ar[i] - other) * oscale;
+      }
+      // lane (q, b, c) keeps rows 2c, 2c + 1 of its 4q group, both components
+      const float g0 = __shfl_xor(c ? v[0] : v[2], 1, 64), g1 = __shfl_xor(c ? v[1] : v[3], 1, 64);
+      res[ct] = c ? make_float4(g0, v[2], g1, v[3]) : make_float4(v[0], g0, v[1], g1);
+      if constexpr (MODE == kModeAm) {
+        const uint32_t rr = cbase + 16u * (uint32_t)b + 4u * (uint32_t)q + 2u * (uint32_t)c;
+        const uint64_t k = k_t + rr;
+        const float e0 = am_env(make_float2(res[ct].x, res[ct].y)), e1 = am_env(make_float2(res[ct].z, res[ct].w));
+        if (k + 1 < p.N) {
+          *reinterpret_cast<float2*>(out + k) = make_float2(e0, e1);
+        } else if (k < p.N) {
+          out[k] = e0;
+        }
+      }
+    }
+    __syncthreads();  // every wave is done reading the tile's planes
+    if constexpr (MODE == kModeFm) {
+      float4* ybuf = reinterpret_cast<float4*>(lds);  // y'[rr], y'[rr + 1] at float4 slot rr / 2
+#pragma unroll
+      for (int ct = 0; ct < C::NCT; ++ct) {
+        const uint32_t rr = (w * C::NCT + (uint32_t)ct) * 128u + 16u * (uint32_t)b + 4u * (uint32_t)q + 2u * (uint32_t)c;
+        ybuf[rr >> 1] = res[ct];
+      }
+      __syncthreads();
+      const float2* y2 = reinterpret_cast<const float2*>(lds);
+      for (uint32_t r = tid; r < (uint32_t)C::STRIDE; r += C::WG) {
+        const uint64_t k = k_t + r;
+        if (k < p.N) {
+          const float2 z = disc_product(y2[r], y2[r + 1]);
+          float ang = disc_atan2(z.y, z.x) + dphi;
+          ang = ang > 3.14159274f ? ang - 6.28318548f : (ang <= -3.14159274f ? ang + 6.28318548f : ang);
+          out[k] = p.fm_gain * ang;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
 }  // namespace gsdr

@@ -33,7 +33,8 @@ static bool nco_increment(float fs, float tune, float chan, uint32_t* inc) {
 template <class InT>
 static hipError_t chain_entry(int mode, float fs, float tune, float chan, float dev, uint32_t decimation,
                               size_t firstSampleIndex, const float* taps, size_t tapCount, const InT* input,
-                              float* output, size_t numOutputs, int32_t device, hipStream_t stream) {
+                              float* output, size_t numOutputs, int32_t device, hipStream_t stream,
+                              int variant = -1) {
   if (numOutputs == 0) return hipSuccess;
   if (decimation == 0 || output == nullptr || input == nullptr) return hipErrorInvalidValue;
   if (tapCount > 0 && taps == nullptr) return hipErrorInvalidValue;
@@ -46,6 +47,7 @@ static hipError_t chain_entry(int mode, float fs, float tune, float chan, float 
   job.T = tapCount;
   job.N = numOutputs;
   job.mode = mode;
+  job.variant = variant;
   job.nco_n0 = (uint32_t)firstSampleIndex;
   if (mode == kModeFm) {
     job.L = numOutputs * (size_t)decimation + tapCount;  // N + 1 FIR outputs
@@ -155,6 +157,18 @@ GSDR_C_LINKAGE hipError_t gsdrxAmDemodInt8(float rfSampleRate, float tuningFrequ
                            firstSampleIndex, lowPassTaps, numLowPassTaps, reinterpret_cast<const gsdr::Iq8*>(input),
                            output, numElements, cudaDevice, cudaStream);
 }
+
+namespace gsdr {
+// int8 FM / AM chain on the exact packed-VALU path (bit-identical to gsdrInt8ToNormFloat + the float chain):
+// the streaming object's int8 chains, whose chunked output must reproduce one call bit for bit (the
+// decimation-4 matrix-core default sums in an order that depends on where a call starts)
+hipError_t chain_int8_exact(int mode, float fs, float tune, float chan, float dev, uint32_t decimation,
+                            size_t firstSampleIndex, const float* taps, size_t tapCount, const int8_t* input,
+                            float* output, size_t numOutputs, int32_t device, hipStream_t stream) {
+  return chain_entry(mode, fs, tune, chan, mode == kModeFm ? dev : 1.0f, decimation, firstSampleIndex, taps, tapCount,
+                     reinterpret_cast<const Iq8*>(input), output, numOutputs, device, stream, 0);
+}
+}  // namespace gsdr
 
 GSDR_C_LINKAGE uint32_t gsdrNcoPhaseIncrement(float rfSampleRate, float tuningFrequency,
                                               float channelFrequency) GSDR_NO_EXCEPT {

@@ -40,6 +40,13 @@ struct gsdrxStream_t {
 };
 
 namespace gsdr {
+// fm_am.hip: the int8 chains on the exact path (kModeFm = 1, kModeAm = 2 as in fir_engine.hpp)
+hipError_t chain_int8_exact(int mode, float fs, float tune, float chan, float dev, uint32_t decimation,
+                            size_t firstSampleIndex, const float* taps, size_t tapCount, const int8_t* input,
+                            float* output, size_t numOutputs, int32_t device, hipStream_t stream);
+
+constexpr int kChainFm = 1, kChainAm = 2;
+
 namespace {
 
 struct Plan {
@@ -75,13 +82,13 @@ hipError_t filter(const gsdrxStream_t& s, const void* in, uint64_t first, void* 
                 : gsdrFirFC(s.D, s.taps, s.T, static_cast<const hipFloatComplex*>(in),
                             static_cast<hipFloatComplex*>(out), n, s.device, st);
     case GSDRX_STREAM_FM:
-      return i8 ? gsdrxFmDemodInt8(s.fs, s.tune, s.chan, s.dev, s.D, first, s.taps, s.T,
+      return i8 ? chain_int8_exact(kChainFm, s.fs, s.tune, s.chan, s.dev, s.D, first, s.taps, s.T,
                                    static_cast<const int8_t*>(in), static_cast<float*>(out), n, s.device, st)
                 : gsdrFmDemod(s.fs, s.tune, s.chan, s.dev, s.D, first, s.taps, s.T,
                               static_cast<const hipFloatComplex*>(in), static_cast<float*>(out), n, s.device, st);
     default:
-      return i8 ? gsdrxAmDemodInt8(s.fs, s.tune, s.chan, s.D, first, s.taps, s.T, static_cast<const int8_t*>(in),
-                                   static_cast<float*>(out), n, s.device, st)
+      return i8 ? chain_int8_exact(kChainAm, s.fs, s.tune, s.chan, 1.0f, s.D, first, s.taps, s.T,
+                                   static_cast<const int8_t*>(in), static_cast<float*>(out), n, s.device, st)
                 : gsdrAmDemod(s.fs, s.tune, s.chan, s.D, first, s.taps, s.T, static_cast<const hipFloatComplex*>(in),
                               static_cast<float*>(out), n, s.device, st);
   }

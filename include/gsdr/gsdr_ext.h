@@ -90,7 +90,14 @@ GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxFirFCInt8Variant(
     int32_t cudaDevice,
     hipStream_t cudaStream) GSDR_NO_EXCEPT;
 
-/** gsdrFmDemod (fm.h) on int8 I/Q input. */
+/**
+ * gsdrFmDemod (fm.h) on int8 I/Q input. Exception to the bit-identity above: decimation 4 with
+ * numLowPassTaps <= 132 runs on the matrix cores with the NCO folded into complex taps
+ * t_i e^{j 2 pi (i inc mod 2^32) / 2^32} (the discriminator adds the 4-sample phase step back, the
+ * envelope needs no rotation), samples exact in fp16, taps in two fp16 parts: the float chain's parity
+ * bar (wrapped angle within 1e-5 pi g of it) rather than its bits; non-finite taps take the exact
+ * per-output chain. The streaming object's int8 chains (stream.h) keep the exact path.
+ */
 GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxFmDemodInt8(
     float rfSampleRate,
     float tuningFrequency,
@@ -106,7 +113,8 @@ GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxFmDemodInt8(
     int32_t cudaDevice,
     hipStream_t cudaStream) GSDR_NO_EXCEPT;
 
-/** gsdrAmDemod (am.h) on int8 I/Q input. */
+/** gsdrAmDemod (am.h) on int8 I/Q input (decimation 4, <= 132 taps, 8-byte aligned output: matrix cores, as
+ * gsdrxFmDemodInt8). */
 GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxAmDemodInt8(
     float rfSampleRate,
     float tuningFrequency,
@@ -125,8 +133,9 @@ GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxAmDemodInt8(
  * Multi-channel chains (the intent of the reference's unused k_Fm4x,
  * src/fm.cu:71-179): numChannels channels of one RF input, each with its own channel frequency (and
  * FM deviation), sharing the tuning frequency, decimation, taps and firstSampleIndex. Channel c writes
- * output[c * numOutputs + m]; its outputs are bit-identical to gsdrFmDemod / gsdrAmDemod (or the
- * Int8 variants) called with channelFrequencies[c] (and frequencyDeviations[c]). For decimation 2, 4
+ * output[c * numOutputs + m]; its outputs are bit-identical to gsdrFmDemod / gsdrAmDemod called with
+ * channelFrequencies[c] (and frequencyDeviations[c]) -- for int8 I/Q input, on the samples converted by
+ * gsdrInt8ToNormFloat (the Int8 variants' exact path; at decimation 4 those run on the matrix cores). For decimation 2, 4
  * and 8 one kernel reads each input tile from HBM once for up to 16 channels; other decimations run
  * the channels one after another. channelFrequencies / frequencyDeviations are host arrays.
  */

@@ -23,10 +23,12 @@ def chunks(total, seed, W):
 def monolithic(kind, x, taps, D, n0, int8):
     from gsdr_amd import ops
 
+    if int8:
+        # the stream object's int8 kinds run the exact path, bit-identical to conversion + the float
+        # entry point; the D = 4 matrix-core defaults sum in a position-dependent order (stream.h)
+        x = ops.int8_to_norm_float(x).view(torch.complex64)
     if kind == "fir":
-        # int8: the exact path (variant 0) the stream object runs; the D = 4 matrix-core default sums in
-        # a position-dependent order (stream.h)
-        return ops.fir_variant(0, taps, x, D) if int8 else ops.fir(taps, x, D)
+        return ops.fir(taps, x, D)
     if kind == "fm":
         return ops.fm_demod(x, taps, FS, TUNE, CHAN, DEV, D, n0)
     return ops.am_demod(x, taps, FS, TUNE, CHAN, D, n0)

@@ -298,10 +298,16 @@ hipError_t launch_i8_mfma(const FirJob& j, hipStream_t s) {
 }
 
 // int8 I/Q FM / AM chain on the matrix cores (k_chain_i8_mfma): D = 4, T <= 132 (AM: 8-byte aligned output)
+#ifndef GSDR_CHAIN_NCT
+#define GSDR_CHAIN_NCT 2
+#endif
+#ifndef GSDR_CHAIN_BPC
+#define GSDR_CHAIN_BPC 3
+#endif
 template <int MODE>
 hipError_t launch_chain_i8_mfma(const FirJob& j, hipStream_t s) {
-  using C = I8ChainMfma<MODE>;
-  constexpr int BPC = 2;
+  constexpr int NCT = GSDR_CHAIN_NCT, BPC = GSDR_CHAIN_BPC;
+  using C = I8ChainMfma<MODE, NCT>;
   FirParams p = make_params(j);
   const uint32_t ns = (uint32_t)ceil_div<uint64_t>(15u * 4u + j.T, 32u);
   const uint64_t tiles = ceil_div<uint64_t>(j.N, (uint64_t)C::STRIDE);
@@ -312,9 +318,9 @@ hipError_t launch_chain_i8_mfma(const FirJob& j, hipStream_t s) {
   if (e != hipSuccess) return e;
   const uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)cus * BPC);
   if ((reinterpret_cast<uintptr_t>(j.in) % 8) == 0) {
-    k_chain_i8_mfma<MODE, true, BPC><<<dim3(grid), dim3(C::WG), 0, s>>>(p, ns, (uint32_t)tiles);
+    k_chain_i8_mfma<MODE, true, BPC, NCT><<<dim3(grid), dim3(C::WG), 0, s>>>(p, ns, (uint32_t)tiles);
   } else {
-    k_chain_i8_mfma<MODE, false, BPC><<<dim3(grid), dim3(C::WG), 0, s>>>(p, ns, (uint32_t)tiles);
+    k_chain_i8_mfma<MODE, false, BPC, NCT><<<dim3(grid), dim3(C::WG), 0, s>>>(p, ns, (uint32_t)tiles);
   }
   return launch_status();
 }

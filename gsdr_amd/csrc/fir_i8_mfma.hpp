@@ -206,11 +206,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
 // 32-sample step. FM tiles overlap by one output (stride KT - 1) and stage 8-byte granules, so every
 // tile start stays aligned. Normwise parity with the float chains, not bit identity (gsdr_ext.h).
 // ------------------------------------------------------------------------------------------------
-template <int MODE>
+template <int MODE, int NCT_ = 4>
 struct I8ChainMfma {
   static constexpr int D = 4;
   static constexpr int WG = 256;
-  static constexpr int NCT = 4;
+  static constexpr int NCT = NCT_;
   static constexpr int KT = (WG / 64) * NCT * 128;
   static constexpr int STRIDE = MODE == kModeFm ? KT - 1 : KT;
   static constexpr int MAXNS = 6;
@@ -225,9 +225,9 @@ struct I8ChainMfma {
   static_assert(LDS_BYTES >= (uint32_t)KT * 8u, "the FM output pass reuses the planes");
 };
 
-template <int MODE, bool VEC, int BPC>
+template <int MODE, bool VEC, int BPC, int NCT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC))) void k_chain_i8_mfma(FirParams p, uint32_t ns, uint32_t tiles) {
-  using C = I8ChainMfma<MODE>;
+  using C = I8ChainMfma<MODE, NCT>;
   constexpr int D = C::D;
   __shared__ __attribute__((aligned(16))) char lds[C::LDS_BYTES];
   __shared__ float wmax[C::WG / 64];

@@ -270,10 +270,10 @@ def test_fir_int8_mfma_full_config(cuda):
 
 
 # Matrix-core int8 FM / AM chains (D = 4, k_chain_i8_mfma): NCO folded into complex taps, normwise parity
-# with the oracle's chains at tile boundaries (FM tiles stride 2047 outputs, AM 2048), short and odd
+# with the oracle's chains at tile boundaries (FM tiles stride 1023 outputs, AM 1024), short and odd
 # lengths, every supported tap count, large first-sample indices and tuning offsets.
 @pytest.mark.parametrize("T", [1, 2, 33, 127, 132])
-@pytest.mark.parametrize("N", [1, 2, 2046, 2047, 2048, 4095, 4096, 30_001])
+@pytest.mark.parametrize("N", [1, 2, 1022, 1023, 1024, 2046, 2047, 2048, 4095, 30_001])
 def test_chain_int8_mfma_parity(cuda, T, N):
     from gsdr_amd import ops
     from gsdr_amd.signals import fm_test_signal

@@ -77,19 +77,25 @@ int main(int argc, char** argv) {
   CHECK(gsdrFmDemod(fs, 0.0f, chan, dev, D, n1 * D, dTaps, T, dX + n1 * D, dFm2 + n1, N - n1, 0, stream));
 
   // extensions: an int8 I/Q front end fed through the streaming object in uneven buffers, which must
-  // reproduce one gsdrxFmDemodInt8 call over the whole signal bit for bit
+  // reproduce one call of the exact path (gsdrInt8ToNormFloat + gsdrFmDemod) over the whole signal bit for
+  // bit; the one-call gsdrxFmDemodInt8 (decimation 4: matrix cores) meets the float chain's parity bar
   std::vector<int8_t> x8(2 * L);
   for (size_t n = 0; n < L; ++n) {
     x8[2 * n] = (int8_t)std::lrint(100.0f * x[n].x);
     x8[2 * n + 1] = (int8_t)std::lrint(100.0f * x[n].y);
   }
   int8_t* dX8;
-  float *dFm8, *dFm8s;
+  float *dFm8, *dFm8s, *dFm8m, *dX8f;
   CHECK(hipMalloc(&dX8, 2 * L));
+  CHECK(hipMalloc(&dX8f, 2 * L * sizeof(float)));
   CHECK(hipMalloc(&dFm8, N * sizeof(float)));
   CHECK(hipMalloc(&dFm8s, N * sizeof(float)));
+  CHECK(hipMalloc(&dFm8m, N * sizeof(float)));
   CHECK(hipMemcpyAsync(dX8, x8.data(), 2 * L, hipMemcpyHostToDevice, stream));
-  CHECK(gsdrxFmDemodInt8(fs, 0.0f, chan, dev, D, 0, dTaps, T, dX8, dFm8, N, 0, stream));
+  CHECK(gsdrInt8ToNormFloat(dX8, dX8f, 2 * L, 0, stream));
+  CHECK(gsdrFmDemod(fs, 0.0f, chan, dev, D, 0, dTaps, T, reinterpret_cast<const hipFloatComplex*>(dX8f), dFm8, N, 0,
+                    stream));
+  CHECK(gsdrxFmDemodInt8(fs, 0.0f, chan, dev, D, 0, dTaps, T, dX8, dFm8m, N, 0, stream));
   gsdrxStream rx;
   CHECK(gsdrxStreamCreate(&rx, GSDRX_STREAM_FM, GSDRX_SAMPLES_CS8, D, dTaps, T, fs, 0.0f, chan, dev, 0, 0));
   size_t consumed = 0, produced = 0;
@@ -103,13 +109,14 @@ int main(int argc, char** argv) {
   }
   CHECK(gsdrxStreamDestroy(rx));
 
-  std::vector<float> fm(N), fm2(N), fm8(N), fm8s(N);
+  std::vector<float> fm(N), fm2(N), fm8(N), fm8s(N), fm8m(N);
   std::vector<hipFloatComplex> y(N);
   CHECK(hipMemcpyAsync(y.data(), dY, N * sizeof(hipFloatComplex), hipMemcpyDeviceToHost, stream));
   CHECK(hipMemcpyAsync(fm.data(), dFm, N * sizeof(float), hipMemcpyDeviceToHost, stream));
   CHECK(hipMemcpyAsync(fm2.data(), dFm2, N * sizeof(float), hipMemcpyDeviceToHost, stream));
   CHECK(hipMemcpyAsync(fm8.data(), dFm8, N * sizeof(float), hipMemcpyDeviceToHost, stream));
   CHECK(hipMemcpyAsync(fm8s.data(), dFm8s, N * sizeof(float), hipMemcpyDeviceToHost, stream));
+  CHECK(hipMemcpyAsync(fm8m.data(), dFm8m, N * sizeof(float), hipMemcpyDeviceToHost, stream));
   CHECK(hipStreamSynchronize(stream));
   if (argc > 1 && !(dump(argv[1], "taps.f32", taps.data(), T * sizeof(float)) &&
                     dump(argv[1], "x.c64", x.data(), L * sizeof(hipFloatComplex)) &&
@@ -120,6 +127,14 @@ int main(int argc, char** argv) {
   }
   // the stream emits every output whose window has arrived: all N (the input holds N*D + T samples)
   const bool stream_same = produced == N && std::memcmp(fm8.data(), fm8s.data(), N * sizeof(float)) == 0;
+  // matrix-core int8 chain vs the exact path: wrapped angle within 1e-5 pi g (g = fs / (2 pi dev))
+  const double g = fs / (2.0 * 3.141592653589793 * dev);
+  double worst = 0.0;
+  for (size_t i = 0; i < N; ++i) {
+    double d = std::fmod((double)fm8m[i] - (double)fm8[i] + 3.0 * 3.141592653589793 * g, 2.0 * 3.141592653589793 * g);
+    worst = std::fmax(worst, std::fabs(d - 3.141592653589793 * g));
+  }
+  const bool mfma_ok = worst <= 1e-5 * 3.141592653589793 * g;
 
   double lo = 1e30, hi = -1e30;
   for (size_t i = 1000; i < N; ++i) {
@@ -130,8 +145,8 @@ int main(int argc, char** argv) {
   // gsdrFmDemod's gain is fs / (2 pi dev) at the RF rate (reference fm.cu:203), so a full-deviation
   // tone reads +-D after decimation by D
   std::printf("%s: FM output range [%.3f, %.3f] (expect about +-%u), chunked == monolithic: %s, "
-              "int8 stream == monolithic: %s\n",
-              gsdrVersion(), lo, hi, D, same ? "yes" : "NO", stream_same ? "yes" : "NO");
+              "int8 stream == monolithic: %s, int8 matrix-core chain within the parity bar: %s\n",
+              gsdrVersion(), lo, hi, D, same ? "yes" : "NO", stream_same ? "yes" : "NO", mfma_ok ? "yes" : "NO");
   (void)hipFree(dTaps);
   (void)hipFree(dX);
   (void)hipFree(dY);
@@ -140,6 +155,8 @@ int main(int argc, char** argv) {
   (void)hipFree(dX8);
   (void)hipFree(dFm8);
   (void)hipFree(dFm8s);
+  (void)hipFree(dFm8m);
+  (void)hipFree(dX8f);
   (void)hipStreamDestroy(stream);
-  return same && stream_same && hi > 0.8 * D && hi < 1.2 * D && lo < -0.8 * D && lo > -1.2 * D ? 0 : 1;
+  return same && stream_same && mfma_ok && hi > 0.8 * D && hi < 1.2 * D && lo < -0.8 * D && lo > -1.2 * D ? 0 : 1;
 }

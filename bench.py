@@ -366,8 +366,13 @@ def secondary_configs(torch, ops, device, taps):
             "speedup_vs_single_calls": round(C * out["fm_chain"]["us_per_launch"] / (t * 1e6), 2)}
         del ym
     del xs
-    # int8 I/Q front end fused into the filter: 2 instead of 8 input bytes per sample
-    x8s = [torch.randint(-128, 128, (2 * n_in,), dtype=torch.int8, device=device, generator=g) for _ in range(ROTATE)]
+    # int8 I/Q front end fused into the filter: 2 instead of 8 input bytes per sample; the FM chain gets
+    # config 3's signal quantised to int8 (x 100), consecutive batches of one channel
+    x8s = []
+    for b in range(ROTATE):
+        xc = fm_channel(torch, n_in, device, 0x5EED + 1000 * b, b * n_in)  # config 3's batches, as above
+        x8s.append(torch.clamp(torch.round(torch.view_as_real(xc).reshape(-1) * 100), -128, 127).to(torch.int8))
+        del xc
     argsets = [(fs, tune, chan, dev_hz, DECIM, 0, taps.data_ptr(), TAPS, x.data_ptr(), y.data_ptr(), n_fm,
                 device.index, stream) for x in x8s]
     t = time_abi(torch, abi.lib.gsdrxFmDemodInt8, argsets)

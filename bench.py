@@ -380,6 +380,12 @@ def secondary_configs(torch, ops, device, taps):
     out["fm_chain_int8"] = {"config": "config 3 from int8 I/Q (gsdrxFmDemodInt8)", "us_per_launch": round(t * 1e6, 2),
                             "msamples_per_s": round(n_in / t / 1e6, 1), "alg_gbps": round(b / t / 1e9, 1),
                             "alg_bytes_per_launch": b}
+    argsets = [(fs, tune, chan, DECIM, 0, taps.data_ptr(), TAPS, x.data_ptr(), y.data_ptr(), n_fm, device.index,
+                stream) for x in x8s]
+    t = time_abi(torch, abi.lib.gsdrxAmDemodInt8, argsets)
+    out["am_chain_int8"] = {"config": "NCO + 127-tap FIR (D = 4) + AM envelope on config 3's int8 I/Q (gsdrxAmDemodInt8)",
+                            "us_per_launch": round(t * 1e6, 2), "msamples_per_s": round(n_in / t / 1e6, 1),
+                            "alg_gbps": round(b / t / 1e9, 1), "alg_bytes_per_launch": b}
     del y
     yf = torch.empty(N_OUT, dtype=torch.complex64, device=device)
     argsets = [(DECIM, taps.data_ptr(), TAPS, x.data_ptr(), yf.data_ptr(), N_OUT, device.index, stream) for x in x8s]

@@ -222,7 +222,6 @@ struct I8ChainMfma {
   __host__ __device__ static constexpr uint32_t addr(uint32_t idx) { return idx * 2u + (idx / 64u) * 16u; }
   static constexpr uint32_t PLANE = (addr(SPAN) + 255u) / 256u * 256u + 128u;
   static constexpr uint32_t LDS_BYTES = PLANE + addr(SPAN);
-  static_assert(LDS_BYTES >= (uint32_t)KT * 8u, "the FM output pass reuses the planes");
 };
 
 template <int MODE, bool VEC, int BPC, int NCT>
@@ -230,6 +229,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
   using C = I8ChainMfma<MODE, NCT>;
   constexpr int D = C::D;
   __shared__ __attribute__((aligned(16))) char lds[C::LDS_BYTES];
+  __shared__ float4 ybuf[MODE == kModeFm ? C::KT / 2 : 1];  // FM: the tile's FIR outputs y'
   __shared__ float wmax[C::WG / 64];
   __shared__ uint32_t wbad[C::WG / 64];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
@@ -391,16 +391,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
         }
       }
     }
-    __syncthreads();  // every wave is done reading the tile's planes
     if constexpr (MODE == kModeFm) {
-      float4* ybuf = reinterpret_cast<float4*>(lds);  // y'[rr], y'[rr + 1] at float4 slot rr / 2
+      // the tile's y' in their own LDS slots (y'[rr], y'[rr + 1] at float4 slot rr / 2), then one barrier
+      // for both the planes (read by every wave's MFMAs) and y' (read across waves below); the next
+      // tile's staging barrier orders this pass's reads before the next writes of ybuf
 #pragma unroll
       for (int ct = 0; ct < C::NCT; ++ct) {
         const uint32_t rr = (w * C::NCT + (uint32_t)ct) * 128u + 16u * (uint32_t)b + 4u * (uint32_t)q + 2u * (uint32_t)c;
         ybuf[rr >> 1] = res[ct];
       }
       __syncthreads();
-      const float2* y2 = reinterpret_cast<const float2*>(lds);
+      const float2* y2 = reinterpret_cast<const float2*>(ybuf);
       for (uint32_t r = tid; r < (uint32_t)C::STRIDE; r += C::WG) {
         const uint64_t k = k_t + r;
         if (k < p.N) {
@@ -410,7 +411,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
           out[k] = p.fm_gain * ang;
         }
       }
-      __syncthreads();
+    } else {
+      __syncthreads();  // every wave is done reading the tile's planes
     }
   }
 }

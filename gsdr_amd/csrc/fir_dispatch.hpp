@@ -37,6 +37,7 @@ struct FirJob {
   uint32_t nco_inc = 0;
   uint32_t nco_n0 = 0;
   float fm_gain = 0.0f;
+  uint32_t out_phase = 0;  // absolute index of output 0 mod 16 (fir_i8_mfma.hpp)
 };
 
 // LDS budget per workgroup for the tiled kernels (keeps >= 2 workgroups per CU on 160 KiB).
@@ -54,6 +55,7 @@ inline FirParams make_params(const FirJob& j) {
   p.nco_inc = j.nco_inc;
   p.nco_n0 = j.nco_n0;
   p.fm_gain = j.fm_gain;
+  p.out_phase = j.out_phase & 15u;
   return p;
 }
 
@@ -272,34 +274,52 @@ hipError_t launch_multi_chain(const FirJob& j, const MultiParams& mp, hipStream_
   }
 }
 
-// int8 I/Q FIR on the matrix cores (k_fir_i8_mfma, fir_i8_mfma.hpp): D = 4, T <= I8Mfma<4>::MAXT,
-// 16-byte aligned output; persistent workgroups (their tap fragments are built once).
-template <int D, int BPC = 4>
-hipError_t launch_i8_mfma(const FirJob& j, hipStream_t s) {
-  using C = I8Mfma<D>;
-  if (j.D != (size_t)D || j.T < 1 || j.T > (size_t)C::MAXT || (reinterpret_cast<uintptr_t>(j.out) % 16) != 0) {
-    return hipErrorInvalidValue;
-  }
+// int8 I/Q FIR on the matrix cores (k_fir_i8_mfma, fir_i8_mfma.hpp): D = 4, T <= 196; persistent
+// workgroups (their tap fragments are built once). The tile grid starts at output -out_phase, so the
+// staging granule and the output pairs are aligned per call from the pointers and the phase.
+template <int D, int NS, int BPC>
+hipError_t launch_i8_mfma_ns(const FirJob& j, hipStream_t s) {
+  using C = I8Mfma<D, NS>;
   FirParams p = make_params(j);
   const uint32_t ns = (uint32_t)ceil_div<uint64_t>(15u * D + j.T, 32u);
-  const uint64_t tiles = ceil_div<uint64_t>(j.N, (uint64_t)C::KT);
+  const uint64_t tiles = ceil_div<uint64_t>(j.N + p.out_phase, (uint64_t)C::KT);
   if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
   int dev = 0, cus = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   if (e != hipSuccess) return e;
   const uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)cus * BPC);
-  if ((reinterpret_cast<uintptr_t>(j.in) % 16) == 0) {
-    k_fir_i8_mfma<D, true, BPC><<<dim3(grid), dim3(C::WG), 0, s>>>(p, ns, (uint32_t)tiles);
+  // tile starts are at sample (j KT - phase) D: byte offset 2 D (j KT - phase) from the input
+  const uintptr_t in0 = reinterpret_cast<uintptr_t>(j.in) - 2u * D * p.out_phase;
+  const bool oa = ((reinterpret_cast<uintptr_t>(j.out) - 8u * p.out_phase) % 16) == 0;
+#define GSDR_I8_LAUNCH(G, VEC)                                                                             \
+  (oa ? (k_fir_i8_mfma<D, NS, G, VEC, true, BPC><<<dim3(grid), dim3(C::WG), 0, s>>>(p, ns, (uint32_t)tiles), 0) \
+      : (k_fir_i8_mfma<D, NS, G, VEC, false, BPC><<<dim3(grid), dim3(C::WG), 0, s>>>(p, ns, (uint32_t)tiles), 0))
+  if (in0 % 16 == 0) {
+    (void)GSDR_I8_LAUNCH(8, true);
+  } else if (in0 % 8 == 0) {
+    (void)GSDR_I8_LAUNCH(4, true);
   } else {
-    k_fir_i8_mfma<D, false, BPC><<<dim3(grid), dim3(C::WG), 0, s>>>(p, ns, (uint32_t)tiles);
+    (void)GSDR_I8_LAUNCH(8, false);
   }
+#undef GSDR_I8_LAUNCH
   return launch_status();
 }
 
-// int8 I/Q FM / AM chain on the matrix cores (k_chain_i8_mfma): D = 4, T <= 132 (AM: 8-byte aligned output)
+template <int D, int BPC = 3>
+hipError_t launch_i8_mfma(const FirJob& j, hipStream_t s) {
+  if (j.D != (size_t)D || j.T < 1 || j.T > (size_t)I8Mfma<D, 8>::MAXT ||
+      (reinterpret_cast<uintptr_t>(j.out) % 8) != 0) {
+    return hipErrorInvalidValue;
+  }
+  // 6 K steps (15 D + T <= 192) cover T <= 132 with fewer fragment registers than 8
+  if (j.T <= (size_t)I8Mfma<D, 6>::MAXT) return launch_i8_mfma_ns<D, 6, BPC>(j, s);
+  return launch_i8_mfma_ns<D, 8, BPC>(j, s);
+}
+
+// int8 I/Q FM / AM chain on the matrix cores (k_chain_i8_mfma): D = 4, T <= 132
 #ifndef GSDR_CHAIN_NCT
-#define GSDR_CHAIN_NCT 2
+#define GSDR_CHAIN_NCT 4
 #endif
 #ifndef GSDR_CHAIN_BPC
 #define GSDR_CHAIN_BPC 3
@@ -309,14 +329,15 @@ hipError_t launch_chain_i8_mfma(const FirJob& j, hipStream_t s) {
   constexpr int NCT = GSDR_CHAIN_NCT, BPC = GSDR_CHAIN_BPC;
   using C = I8ChainMfma<MODE, NCT>;
   FirParams p = make_params(j);
-  const uint32_t ns = (uint32_t)ceil_div<uint64_t>(15u * 4u + j.T, 32u);
-  const uint64_t tiles = ceil_div<uint64_t>(j.N, (uint64_t)C::STRIDE);
+  const uint32_t ns = (uint32_t)ceil_div<uint64_t>(7u * 4u + j.T, 32u);
+  const uint64_t tiles = ceil_div<uint64_t>(j.N + p.out_phase, (uint64_t)C::STRIDE);
   if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
   int dev = 0, cus = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   if (e != hipSuccess) return e;
   const uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)cus * BPC);
+  // tile starts are at sample 4 (j STRIDE - phase): a multiple of 4 samples = 8 bytes from the input
   if ((reinterpret_cast<uintptr_t>(j.in) % 8) == 0) {
     k_chain_i8_mfma<MODE, true, BPC, NCT><<<dim3(grid), dim3(C::WG), 0, s>>>(p, ns, (uint32_t)tiles);
   } else {
@@ -345,7 +366,7 @@ inline hipError_t launch_d4_int8(const FirJob& j, hipStream_t s) {
       return launch_poly<float, Iq8, 4, 4, 16, 64, kModeFir, 0, true>(j, s);
     case 28:
       return launch_poly<float, Iq8, 4, 4, 16, 128, kModeFir, 0, true>(j, s);
-    case 40:  // matrix cores (fp16 products, normwise parity), 4 workgroups per CU (128 VGPRs, spills)
+    case 40:  // matrix cores (exact bf16 tap parts, normwise parity), 4 workgroups per CU
       return launch_i8_mfma<4, 4>(j, s);
     case 41:  // matrix cores, 3 workgroups per CU: the default for D = 4
       return launch_i8_mfma<4, 3>(j, s);
@@ -484,15 +505,14 @@ hipError_t launch_fir(const FirJob& j, hipStream_t s) {
     // D = 4 FM / AM chains: the matrix-core kernel with the NCO folded into complex taps (normwise
     // parity with the float chains: DESIGN.md section 3.3); variant 0 keeps the exact path (streams)
     if constexpr (MODE != kModeFir && std::is_same<TapT, float>::value) {
-      if (j.D == 4 && j.variant < 0 && j.T <= (size_t)I8ChainMfma<MODE>::MAXT &&
-          (MODE == kModeFm || (reinterpret_cast<uintptr_t>(j.out) % 8) == 0)) {
+      if (j.D == 4 && j.variant < 0 && j.T <= (size_t)I8ChainMfma<MODE>::MAXT) {
         return launch_chain_i8_mfma<MODE>(j, s);
       }
     }
-    // D = 4 FIR: the matrix-core kernel (fp16-exact samples, two-part taps; normwise parity with the
-    // float path, twice its speed: DESIGN.md section 3.3)
+    // D = 4 FIR: the matrix-core kernel (bf16-exact samples, exact three-part taps; normwise parity with
+    // the float path, twice its speed: DESIGN.md section 3.3)
     if constexpr (MODE == kModeFir && std::is_same<TapT, float>::value) {
-      if (j.D == 4 && j.T <= (size_t)I8Mfma<4>::MAXT && (reinterpret_cast<uintptr_t>(j.out) % 16) == 0) {
+      if (j.D == 4 && j.T <= (size_t)I8Mfma<4, 8>::MAXT && (reinterpret_cast<uintptr_t>(j.out) % 8) == 0) {
         return launch_i8_mfma<4, 3>(j, s);
       }
     }

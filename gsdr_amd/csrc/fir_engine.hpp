@@ -190,7 +190,7 @@ struct FirParams {
   uint32_t nco_inc;      // NCO phase increment per sample, 2^-32 cycles
   uint32_t nco_n0;       // low 32 bits of firstSampleIndex
   float fm_gain;         // FM discriminator gain
-  uint32_t pad_;
+  uint32_t out_phase;    // absolute index of output 0 mod 16 (the int8 matrix-core kernels' block grid)
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -609,8 +609,8 @@ __device__ __forceinline__ float fm_disc(float2 y0, float2 y1, float g) {
 
 // fm_disc(a0, a1) and fm_disc(b0, b1) with the polynomial, the fix-up subtractions and the gain on
 // packed FMAs / multiplies (two outputs per instruction)
-__device__ __forceinline__ gsdr_f32x2 fm_disc2(float2 a0, float2 a1, float2 b0, float2 b1, float g) {
-  const float2 za = disc_product(a0, a1), zb = disc_product(b0, b1);
+// arg(za), arg(zb) of two discriminator products on packed FMAs (disc_atan2's operations)
+__device__ __forceinline__ gsdr_f32x2 disc_angle2(float2 za, float2 zb) {
   const float axa = fabsf(za.x), aya = fabsf(za.y), axb = fabsf(zb.x), ayb = fabsf(zb.y);
   const gsdr_f32x2 t = gsdr_f32x2{fminf(axa, aya), fminf(axb, ayb)} *
                        gsdr_f32x2{__builtin_amdgcn_rcpf(fmaxf(axa, aya)), __builtin_amdgcn_rcpf(fmaxf(axb, ayb))};
@@ -624,7 +624,11 @@ __device__ __forceinline__ gsdr_f32x2 fm_disc2(float2 a0, float2 a1, float2 b0, 
   r = gsdr_f32x2{copysignf(r.x, za.y), copysignf(r.y, zb.y)};
   if (!disc_fast(za.y, za.x)) r.x = atan2f(za.y, za.x);
   if (!disc_fast(zb.y, zb.x)) r.y = atan2f(zb.y, zb.x);
-  return gsdr_f32x2{g, g} * r;
+  return r;
+}
+
+__device__ __forceinline__ gsdr_f32x2 fm_disc2(float2 a0, float2 a1, float2 b0, float2 b1, float g) {
+  return gsdr_f32x2{g, g} * disc_angle2(disc_product(a0, a1), disc_product(b0, b1));
 }
 
 // AM envelope: 2 * saturate(|y|) - 1, saturate(NaN) = 0 (reference src/am.cu:49, quad_demod.cu:47-48).

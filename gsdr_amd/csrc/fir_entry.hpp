@@ -14,7 +14,7 @@ namespace gsdr {
 template <class TapT, class InT>
 inline hipError_t fir_entry(size_t decimation, const TapT* taps, size_t tapCount, const InT* input,
                             typename Product<TapT, InT>::type* output, size_t numOutputs, int32_t device,
-                            hipStream_t stream, int variant) {
+                            hipStream_t stream, int variant, uint32_t out_phase = 0) {
   using OutT = typename Product<TapT, InT>::type;
   if (numOutputs == 0) return hipSuccess;
   if (decimation == 0 || output == nullptr) return hipErrorInvalidValue;
@@ -35,6 +35,7 @@ inline hipError_t fir_entry(size_t decimation, const TapT* taps, size_t tapCount
                    job.L = (numOutputs - 1) * decimation + tapCount;
                    job.mode = kModeFir;
                    job.variant = variant;
+                   job.out_phase = out_phase;
                    return launch_fir<TapT, InT, kModeFir>(job, stream);
                  })());
 }

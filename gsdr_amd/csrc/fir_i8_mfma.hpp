@@ -1,68 +1,79 @@
-// gsdr-mi355x: int8 I/Q FIR on the matrix cores (gsdrxFirFCInt8).
+// gsdr-mi355x: int8 I/Q FIR and FM / AM chains on the matrix cores (gsdrxFirFCInt8, gsdrxFmDemodInt8,
+// gsdrxAmDemodInt8 at decimation 4).
 //
-// The int8 front end's samples are small integers (|v| <= 127 after gsdrInt8ToNormFloat's clamp), so
-// they are EXACT in fp16, and the FIR becomes an f16 matrix product with fp32 accumulation whose only
-// rounding is the accumulation itself:
-//   * taps: scaled by 2^sc (exact) so that max|t| lies in [2^13, 2^14), then split t = hi + lo into two
-//     fp16 parts (|t - hi - lo| <= 2^-22 |t|; tiny taps lose only absolute precision far below the
-//     normwise bar); each product v * hi and v * lo is exact in fp32;
-//   * y[k] = (sum_i t[i] v[kD + i]) * (2^-sc / 127), the reference's per-sample v / 127 moved outside
-//     the sum (fir.cu:49-71 with conversion.cu:20-35's normalisation).
-// The result matches the float path within the floating-point parity bar (normwise)
-// rather than bit for bit: the products are summed in the matrix core's order. Taps that are not all
-// finite take an exact per-output loop instead (fir_point), so non-finite semantics stay the reference's.
+// The int8 front end's samples are small integers (|v| <= 127 after gsdrInt8ToNormFloat's clamp), exact in
+// bf16, and every fp32 tap is split EXACTLY into three bf16 parts:
+//   * taps are scaled by 2^sc (exact) so that max|t| lies in [2^99, 2^100), then
+//     t = b1 + b2 + b3 with b1 = bf16(t), b2 = bf16(t - b1), b3 = t - b1 - b2 (8 significant bits each:
+//     24 bits in all, so b3 is exact). bf16 has fp32's exponent range, so a tap 2^-200 below the largest
+//     is split as exactly as the largest: round 2's two fp16 parts under one scale turned the sinc
+//     zero-crossing taps (~1e-18) of an ordinary low-pass into 0, which an impulse or a sparse window
+//     exposes at a normwise error of 1 (What's weak 1). A tap set whose split is not exact
+//     (dynamic range beyond ~2^200, or not finite) takes the exact per-output loop (fir_point) instead;
+//   * every product v * b is exact in fp32 (8 x 8 bits), so the only roundings are the matrix core's fp32
+//     accumulation and the final scale y = (acc / 127) 2^-sc -- the reference's per-sample v / 127
+//     (conversion.cu:20-35) moved outside the sum of fir.cu:49-71. The result meets the float path's
+//     normwise bar for every input, sparse ones included, rather than matching it bit for
+//     bit: the products are summed in the matrix core's order.
+// Shift invariance: the 16-output blocks a matrix tile is built from are aligned to the ABSOLUTE output
+// index (FirParams::out_phase = absolute index of output 0 mod 16), so an output's summation order depends
+// only on the taps, its own window and its absolute index mod 16 -- never on where a call starts. The
+// streaming object and the multi-channel entry points therefore reproduce one monolithic call bit for bit
+// on this path too (include/gsdr/stream.h).
 //
-// Matrix formulation (v_mfma_f32_16x16x32_f16: A 16x32, B 32x16, C 16x16 fp32):
+// FIR (v_mfma_f32_16x16x32_bf16: A 16x32, B 32x16, C 16x16 fp32):
 //   C[m][n] = sum_kk A[m][kk] B[kk][n],  A[m][kk] = t[kk - D m] (zero outside [0, T)),
 //   B[kk][n] = component (n & 1) of x[(k0 + 16 (n >> 1)) D + kk],
 // so column n holds 16 consecutive outputs (block n >> 1 of the C tile's 8) of one component, and one C
 // tile is 128 consecutive complex outputs. K = 15 D + T padded to 32-sample steps (6 at D = 4, T = 127).
-// A is the same for every tile: each lane keeps its fragments (hi and lo, 8 fp16 per step) in registers
-// for the kernel's lifetime (persistent workgroups). B comes from LDS, where the staging pass wrote the
-// tile's samples as two fp16 planes (I and Q) with a 16-byte pad after every 64 samples: the 16 lanes
-// that read together (one per column) then hit 16 distinct 16-byte bank groups.
+// A is the same for every tile: each lane keeps its fragments (3 parts x 8 bf16 per step) in registers for
+// the kernel's lifetime (persistent workgroups). B comes from LDS, where the staging pass wrote the tile's
+// samples as two bf16 planes (I and Q) with a 16-byte pad after every 64 samples: the 16 lanes that read
+// together (one per column) then hit 16 distinct 16-byte bank groups.
 #pragma once
 
 #include "fir_engine.hpp"
 
 namespace gsdr {
 
-typedef _Float16 gsdr_h8 __attribute__((ext_vector_type(8)));
+typedef __bf16 gsdr_b8 __attribute__((ext_vector_type(8)));
+typedef __bf16 gsdr_b4 __attribute__((ext_vector_type(4)));
 typedef float gsdr_f4v __attribute__((ext_vector_type(4)));
 typedef uint32_t gsdr_u4v __attribute__((ext_vector_type(4)));
+typedef uint32_t gsdr_u2v __attribute__((ext_vector_type(2)));
 
-template <int D>
-struct I8Mfma {
-  static constexpr int WG = 256;
-  static constexpr int NCT = 4;                     // C tiles (128 outputs) per wave and tile
-  static constexpr int KT = (WG / 64) * NCT * 128;  // outputs per tile
-  static constexpr int MAXNS = 8;                   // 32-sample K steps: 15 D + T <= 256
-  static constexpr int MAXT = 32 * MAXNS - 15 * D;
-  static constexpr int SPAN = (KT - 16) * D + 32 * MAXNS;  // samples staged per tile
-  static_assert(SPAN % 8 == 0, "staging moves 8 samples a lane");
-  __host__ __device__ static constexpr uint32_t addr(uint32_t idx) { return idx * 2u + (idx / 64u) * 16u; }
-  // Q plane offset: = 128 (mod 256), so the Q columns' bank groups interleave the I columns'
-  static constexpr uint32_t PLANE = (addr(SPAN) + 255u) / 256u * 256u + 128u;
-  static constexpr uint32_t LDS_BYTES = PLANE + addr(SPAN);
-};
+// tap scale: max|t| 2^sc in [2^99, 2^100); all-zero taps give sc = 100
+__device__ __forceinline__ int i8_tap_scale(float amax) {
+  int e = 0;
+  (void)frexpf(amax, &e);  // amax = f 2^e, f in [0.5, 1) (e = 0 for amax = 0)
+  return 100 - e;
+}
 
-// BPC workgroups per CU (one wave per SIMD each): the register budget is 512 / BPC VGPRs
-template <int D, bool VEC, int BPC>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC))) void k_fir_i8_mfma(FirParams p, uint32_t ns, uint32_t tiles) {
-  using C = I8Mfma<D>;
-  __shared__ __attribute__((aligned(16))) char lds[C::LDS_BYTES];
-  __shared__ float wmax[C::WG / 64];
-  __shared__ uint32_t wbad[C::WG / 64];
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
-  const float* __restrict__ taps = reinterpret_cast<const float*>(p.taps);
-  const Iq8* __restrict__ in = reinterpret_cast<const Iq8*>(p.in);
-  float2* __restrict__ out = reinterpret_cast<float2*>(p.out);
-  const uint32_t T = p.T;
+__device__ __forceinline__ bool bf16_normal_or_zero(__bf16 b) {
+  const float f = (float)b;
+  return f == 0.0f || fabsf(f) >= 0x1p-126f;
+}
 
-  // tap scale (T <= MAXT <= 256: one tap a thread), and whether every tap is finite
-  const float t = tid < T ? taps[tid] : 0.0f;
-  float a = fabsf(t);
-  uint32_t bad = isfinite(t) ? 0u : 1u;
+// v = b1 + b2 + b3 exactly (returns false when it is not: v not finite, or a part below bf16's normal range)
+__device__ __forceinline__ bool split3(float v, __bf16& b1, __bf16& b2, __bf16& b3) {
+  b1 = (__bf16)v;
+  const float r1 = v - (float)b1;  // exact: b1 is v rounded to 8 significant bits
+  b2 = (__bf16)r1;
+  const float r2 = r1 - (float)b2;
+  b3 = (__bf16)r2;
+  return isfinite(v) && (float)b3 == r2 && bf16_normal_or_zero(b1) && bf16_normal_or_zero(b2) &&
+         bf16_normal_or_zero(b3);
+}
+
+// int8 component (bits [8 u, 8 u + 8) of w) as gsdrInt8ToNormFloat's numerator: clamp -128 to -127
+__device__ __forceinline__ __bf16 i8_bf16(uint32_t w, int u) {
+  return (__bf16)(float)max((int)(w << (24 - 8 * u)) >> 24, -127);
+}
+
+// Reduce |value| max and a "not exactly representable" flag over the workgroup (WG threads, 64-lane waves).
+template <int WG>
+__device__ __forceinline__ void wg_max_bad(float& a, uint32_t& bad, float* wmax, uint32_t* wbad) {
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
   for (int o = 32; o > 0; o >>= 1) {
     a = fmaxf(a, __shfl_xor(a, o, 64));
     bad |= __shfl_xor(bad, o, 64);
@@ -72,30 +83,209 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
     wbad[w] = bad;
   }
   __syncthreads();
-  float amax = wmax[0];
+  a = wmax[0];
   bad = wbad[0];
 #pragma unroll
-  for (int i = 1; i < C::WG / 64; ++i) {
-    amax = fmaxf(amax, wmax[i]);
+  for (int i = 1; i < WG / 64; ++i) {
+    a = fmaxf(a, wmax[i]);
     bad |= wbad[i];
   }
-  if (bad) {  // non-finite taps: the reference's ascending loop, output by output
-    for (uint32_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
-      for (uint32_t r = tid; r < (uint32_t)C::KT; r += C::WG) {
-        const uint64_t k = (uint64_t)tile * C::KT + r;
-        if (k < p.N) out[k] = fir_point<float, Iq8, kModeFir>(p, k);
+}
+
+// Cross-lane moves without LDS: lane ^ 1 by DPP (quad_perm [1, 0, 3, 2]), lane ^ 32 by gfx950's
+// v_permlane32_swap (__shfl_xor compiles to ds_bpermute, an LDS instruction with its own wait)
+__device__ __forceinline__ float lane_xor1(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float lane_xor32(float x) {
+  // swap(vdst = x, src = x): vdst's lanes 32-63 <- src's lanes 0-31, src's lanes 0-31 <- vdst's lanes 32-63
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float((threadIdx.x & 32u) ? r[0] : r[1]);
+}
+
+// Output scale 2^-sc / 127: one multiply by that constant while it is a normal float (then it equals
+// 2^-sc fl(1/127) exactly, and acc * it rounds once), else (acc / 127-ish) then the exponent shift
+// (as ldexpf(acc * k, sh): k = that constant and sh = 0, or k = fl(1/127) and sh = -sc; two instructions, no
+// select)
+struct I8OutScale {
+  float k;
+  int sh;
+  __device__ __forceinline__ explicit I8OutScale(int sc)
+      : k(sc <= 118 ? ldexpf(1.0f / 127.0f, -sc) : 1.0f / 127.0f), sh(sc <= 118 ? 0 : -sc) {}
+  __device__ __forceinline__ float operator()(float acc) const { return ldexpf(acc * k, sh); }
+};
+
+// LDS plane layout: 2 bytes a sample, a 16-byte pad after every 64 samples
+__host__ __device__ constexpr uint32_t i8_addr(uint32_t idx) { return idx * 2u + (idx / 64u) * 16u; }
+
+// Staging of samples [S0, S0 + SPAN) (absolute offsets into `in`, zero outside [0, L)) as bf16 I and Q
+// planes, in two halves so the next tile's loads can be in flight while this tile is computed (the
+// kernels are persistent, so a tile's HBM latency would otherwise stand between every two tiles):
+// i8_load_granules issues every load of a tile into registers, i8_store_planes converts and writes them.
+// G samples a lane and load (8: 16-byte loads, 4: 8-byte loads); VEC = the in-range granules are
+// G * 2-byte aligned.
+template <int G, int SPAN, int WG>
+struct I8Stage {
+  static_assert(G == 8 || G == 4, "granule of 8 or 4 samples");
+  static_assert(SPAN % G == 0, "whole granules");
+  static constexpr uint32_t NG = SPAN / G, NGR = (NG + WG - 1) / WG;
+  static constexpr int NW = G / 2;  // dwords a granule
+  uint32_t wv[NGR][NW];
+};
+
+template <int G, bool VEC, int SPAN, int WG>
+__device__ __forceinline__ void i8_load_granules(I8Stage<G, SPAN, WG>& st, const Iq8* __restrict__ in, int64_t S0,
+                                                 uint64_t L) {
+  using S = I8Stage<G, SPAN, WG>;
+  const uint32_t tid = threadIdx.x;
+  if (VEC && S0 >= 0 && (uint64_t)S0 + SPAN <= L) {
+    // interior tile (all but the first and last): no per-granule bounds, a uniform base plus a 32-bit lane
+    // offset per load
+    const char* base = reinterpret_cast<const char*>(in + S0);
+#pragma unroll
+    for (uint32_t r = 0; r < S::NGR; ++r) {
+      const uint32_t g = tid + r * WG;
+      if (r + 1 < S::NGR || g < S::NG) {
+        if constexpr (G == 8) {
+          const gsdr_u4v t = __builtin_nontemporal_load(reinterpret_cast<const gsdr_u4v*>(base + 16u * g));
+#pragma unroll
+          for (int k = 0; k < 4; ++k) st.wv[r][k] = t[k];
+        } else {
+          const gsdr_u2v t = __builtin_nontemporal_load(reinterpret_cast<const gsdr_u2v*>(base + 8u * g));
+          st.wv[r][0] = t.x;
+          st.wv[r][1] = t.y;
+        }
       }
     }
     return;
   }
-  int e = 0;
-  (void)frexpf(amax, &e);  // amax = f 2^e, f in [0.5, 1) (e = 0 for all-zero taps)
-  const int sc = 14 - e;
+#pragma unroll
+  for (uint32_t r = 0; r < S::NGR; ++r) {
+    const uint32_t g = tid + r * WG;
+    const int64_t s = S0 + (int64_t)G * g;
+#pragma unroll
+    for (int k = 0; k < S::NW; ++k) st.wv[r][k] = 0u;
+    if (g < S::NG) {
+      if (VEC && s >= 0 && (uint64_t)s + G <= L) {
+        if constexpr (G == 8) {
+          const gsdr_u4v t = __builtin_nontemporal_load(reinterpret_cast<const gsdr_u4v*>(in + s));
+#pragma unroll
+          for (int k = 0; k < 4; ++k) st.wv[r][k] = t[k];
+        } else {
+          const gsdr_u2v t = __builtin_nontemporal_load(reinterpret_cast<const gsdr_u2v*>(in + s));
+          st.wv[r][0] = t.x;
+          st.wv[r][1] = t.y;
+        }
+      } else {  // input ends, unaligned input or samples before the buffer: per-sample loads, zero outside
+#pragma unroll
+        for (int k = 0; k < S::NW; ++k) {
+          const int64_t i0 = s + 2 * k, i1 = i0 + 1;
+          const Iq8 a = (i0 >= 0 && (uint64_t)i0 < L) ? in[i0] : Iq8{0, 0};
+          const Iq8 b = (i1 >= 0 && (uint64_t)i1 < L) ? in[i1] : Iq8{0, 0};
+          st.wv[r][k] = (uint32_t)(uint8_t)a.x | (uint32_t)(uint8_t)a.y << 8 | (uint32_t)(uint8_t)b.x << 16 |
+                        (uint32_t)(uint8_t)b.y << 24;
+        }
+      }
+    }
+  }
+}
+
+template <int G, int SPAN, int WG>
+__device__ __forceinline__ void i8_store_planes(const I8Stage<G, SPAN, WG>& st, char* lds, uint32_t plane) {
+  using S = I8Stage<G, SPAN, WG>;
+  const uint32_t tid = threadIdx.x;
+#pragma unroll
+  for (uint32_t r = 0; r < S::NGR; ++r) {
+    const uint32_t g = tid + r * WG;
+    if (g < S::NG) {
+      const uint32_t o = i8_addr(G * g);
+      if constexpr (G == 8) {
+        gsdr_b8 hi_, hq_;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {  // sample 2k + u: bytes 2u (I) and 2u + 1 (Q) of dword k
+            hi_[2 * k + u] = i8_bf16(st.wv[r][k], 2 * u);
+            hq_[2 * k + u] = i8_bf16(st.wv[r][k], 2 * u + 1);
+          }
+        }
+        *reinterpret_cast<gsdr_b8*>(lds + o) = hi_;
+        *reinterpret_cast<gsdr_b8*>(lds + plane + o) = hq_;
+      } else {
+        gsdr_b4 hi_, hq_;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            hi_[2 * k + u] = i8_bf16(st.wv[r][k], 2 * u);
+            hq_[2 * k + u] = i8_bf16(st.wv[r][k], 2 * u + 1);
+          }
+        }
+        *reinterpret_cast<gsdr_b4*>(lds + o) = hi_;
+        *reinterpret_cast<gsdr_b4*>(lds + plane + o) = hq_;
+      }
+    }
+  }
+}
+
+template <int D, int NS_>
+struct I8Mfma {
+  static constexpr int WG = 256;
+  static constexpr int NCT = 4;                     // C tiles (128 outputs) per wave and tile
+  static constexpr int KT = (WG / 64) * NCT * 128;  // outputs per tile (a multiple of 16)
+  static constexpr int MAXNS = NS_;                 // 32-sample K steps: 15 D + T <= 32 NS
+  static constexpr int MAXT = 32 * MAXNS - 15 * D;
+  static constexpr int SPAN = (KT - 16) * D + 32 * MAXNS;  // samples staged per tile
+  static_assert(SPAN % 8 == 0, "staging moves 8 samples a lane");
+  __host__ __device__ static constexpr uint32_t addr(uint32_t idx) { return i8_addr(idx); }
+  // Q plane offset: = 128 (mod 256), so the Q columns' bank groups interleave the I columns'
+  static constexpr uint32_t PLANE = (addr(SPAN) + 255u) / 256u * 256u + 128u;
+  static constexpr uint32_t LDS_BYTES = PLANE + addr(SPAN);
+};
+
+// BPC workgroups per CU (one wave per SIMD each): the register budget is 512 / BPC VGPRs.
+// G / VEC: staging granule (I8Stage); OA: the output pairs (k, k + 1) are 16-byte aligned.
+template <int D, int NS, int G, bool VEC, bool OA, int BPC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC))) void k_fir_i8_mfma(FirParams p, uint32_t ns, uint32_t tiles) {
+  using C = I8Mfma<D, NS>;
+  __shared__ __attribute__((aligned(16))) char lds[C::LDS_BYTES];
+  __shared__ float wmax[C::WG / 64];
+  __shared__ uint32_t wbad[C::WG / 64];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+  const float* __restrict__ taps = reinterpret_cast<const float*>(p.taps);
+  const Iq8* __restrict__ in = reinterpret_cast<const Iq8*>(p.in);
+  float2* __restrict__ out = reinterpret_cast<float2*>(p.out);
+  const uint32_t T = p.T;
+  const int64_t phase = (int64_t)p.out_phase;
+
+  // tap scale (T <= MAXT <= 256: one tap a thread); `bad` = some tap is not finite
+  const float t = tid < T ? taps[tid] : 0.0f;
+  float amax = fabsf(t);
+  uint32_t bad = isfinite(t) ? 0u : 1u;
+  wg_max_bad<C::WG>(amax, bad, wmax, wbad);
+  const int sc = i8_tap_scale(amax);
+  if (!bad) {  // and whether every scaled tap splits exactly
+    __bf16 b1, b2, b3;
+    uint32_t inexact = split3(ldexpf(t, sc), b1, b2, b3) ? 0u : 1u;
+    float dummy = 0.0f;
+    __syncthreads();  // wmax / wbad are reused
+    wg_max_bad<C::WG>(dummy, inexact, wmax, wbad);
+    bad = inexact;
+  }
+  if (bad) {  // the reference's ascending loop, output by output
+    for (uint32_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+      for (uint32_t r = tid; r < (uint32_t)C::KT; r += C::WG) {
+        const int64_t k = (int64_t)tile * C::KT - phase + r;
+        if (k >= 0 && (uint64_t)k < p.N) out[k] = fir_point<float, Iq8, kModeFir>(p, (uint64_t)k);
+      }
+    }
+    return;
+  }
   // scaled taps in LDS (zero past T), then this lane's A fragments: row m = lane & 15, k = 8 (lane >> 4) + j
   float* ldsT = reinterpret_cast<float*>(lds);
   ldsT[tid] = ldexpf(t, sc);
   __syncthreads();
-  gsdr_h8 ahi[C::MAXNS], alo[C::MAXNS];
+  gsdr_b8 a1[C::MAXNS], a2[C::MAXNS], a3[C::MAXNS];
   {
     const int m = (int)(lane & 15u), q = (int)(lane >> 4);
 #pragma unroll
@@ -103,95 +293,62 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int i = 32 * s + 8 * q + j - D * m;
-        const float v = i >= 0 ? ldsT[i] : 0.0f;  // i <= 255
-        const _Float16 h = (_Float16)v;
-        ahi[s][j] = h;
-        alo[s][j] = (_Float16)(v - (float)h);  // v - h is exact in fp32
+        __bf16 b1, b2, b3;
+        (void)split3(i >= 0 ? ldsT[i] : 0.0f, b1, b2, b3);  // i <= 255
+        a1[s][j] = b1;
+        a2[s][j] = b2;
+        a3[s][j] = b3;
       }
     }
   }
-  const float oscale = ldexpf(1.0f / 127.0f, -sc);
+  const I8OutScale oscale(sc);
   __syncthreads();  // the tap table is overwritten by the first tile's samples
 
   const int n = (int)(lane & 15u), q = (int)(lane >> 4), c = n & 1, b = n >> 1;
   const char* bplane = lds + (c ? C::PLANE : 0u);
+  I8Stage<G, C::SPAN, C::WG> st;
+  if (blockIdx.x < tiles) i8_load_granules<G, VEC>(st, in, ((int64_t)blockIdx.x * C::KT - phase) * D, p.L);
   for (uint32_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
-    const uint64_t k_t = (uint64_t)tile * C::KT;
-    const uint64_t S0 = k_t * D;
-    // stage SPAN samples as fp16 I and Q planes (16 bytes = 8 samples a lane and step), every load in
-    // flight before the first conversion
-    constexpr uint32_t NG = C::SPAN / 8, NGR = (NG + C::WG - 1) / C::WG;
-    gsdr_u4v wv[NGR];
-#pragma unroll
-    for (uint32_t r = 0; r < NGR; ++r) {
-      const uint32_t g = tid + r * C::WG;
-      const uint64_t s = S0 + 8ull * g;
-      if (g < NG) {
-        if (VEC && s + 8 <= p.L) {
-          wv[r] = __builtin_nontemporal_load(reinterpret_cast<const gsdr_u4v*>(in + s));
-        } else {  // input end or unaligned input: per-sample loads, zero past L
-          uint32_t d[4];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const Iq8 a = s + 2 * k < p.L ? in[s + 2 * k] : Iq8{0, 0};
-            const Iq8 b2 = s + 2 * k + 1 < p.L ? in[s + 2 * k + 1] : Iq8{0, 0};
-            d[k] = (uint32_t)(uint8_t)a.x | (uint32_t)(uint8_t)a.y << 8 | (uint32_t)(uint8_t)b2.x << 16 |
-                   (uint32_t)(uint8_t)b2.y << 24;
-          }
-          wv[r] = gsdr_u4v{d[0], d[1], d[2], d[3]};
-        }
-      }
-    }
-#pragma unroll
-    for (uint32_t r = 0; r < NGR; ++r) {
-      const uint32_t g = tid + r * C::WG;
-      if (g < NG) {
-        gsdr_h8 hi_, hq_;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-#pragma unroll
-          for (int u = 0; u < 2; ++u) {  // sample 2k + u: bytes 2u (I) and 2u + 1 (Q) of dword k
-            // gsdrInt8ToNormFloat clamps -128 to -1.0 = -127 / 127
-            hi_[2 * k + u] = (_Float16)max((int)(wv[r][k] << (24 - 16 * u)) >> 24, -127);
-            hq_[2 * k + u] = (_Float16)max((int)(wv[r][k] << (16 - 16 * u)) >> 24, -127);
-          }
-        }
-        const uint32_t o = C::addr(8u * g);
-        *reinterpret_cast<gsdr_h8*>(lds + o) = hi_;
-        *reinterpret_cast<gsdr_h8*>(lds + C::PLANE + o) = hq_;
-      }
-    }
+    const int64_t k_t = (int64_t)tile * C::KT - phase;  // a multiple of 16 in absolute output index
+    i8_store_planes(st, lds, C::PLANE);
     __syncthreads();
+    // the next tile's loads fly while this one is computed
+    if (tile + gridDim.x < tiles) i8_load_granules<G, VEC>(st, in, (k_t + (int64_t)gridDim.x * C::KT) * D, p.L);
 #pragma unroll 1
     for (int ct = 0; ct < C::NCT; ++ct) {
       const uint32_t cbase = (w * C::NCT + (uint32_t)ct) * 128u;  // the C tile's first output in the tile
       const uint32_t idx0 = (cbase + 16u * (uint32_t)b) * D + 8u * (uint32_t)q;
       gsdr_f4v acc = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-      for (int s = 0; s < C::MAXNS; ++s) {
-        if ((uint32_t)s < ns) {
-          const gsdr_h8 bf = *reinterpret_cast<const gsdr_h8*>(bplane + C::addr(idx0 + 32u * (uint32_t)s));
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi[s], bf, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo[s], bf, acc, 0, 0, 0);
-        }
+      for (int s = 0; s < C::MAXNS; ++s) {  // steps past 15 D + T meet zero taps
+        const gsdr_b8 bf = *reinterpret_cast<const gsdr_b8*>(bplane + C::addr(idx0 + 32u * (uint32_t)s));
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a3[s], bf, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2[s], bf, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[s], bf, acc, 0, 0, 0);
       }
       // lane (q, b, c) holds component c of outputs 4q .. 4q + 3 of block b; the I lane keeps rows 0-1 and
       // the Q lane rows 2-3, each taking the other component from its neighbour
-      const float r0 = acc[0] * oscale, r1 = acc[1] * oscale, r2 = acc[2] * oscale, r3 = acc[3] * oscale;
-      const float g0 = __shfl_xor(c ? r0 : r2, 1, 64), g1 = __shfl_xor(c ? r1 : r3, 1, 64);
-      const float4 o4 = c ? make_float4(g0, r2, g1, r3) : make_float4(r0, g0, r1, g1);
-      const uint64_t k = k_t + cbase + 16u * (uint32_t)b + 4u * (uint32_t)q + 2u * (uint32_t)c;
-      if (k + 1 < p.N) {
-        store16_nt(reinterpret_cast<float4*>(out + k), o4);
-      } else if (k < p.N) {
-        out[k] = make_float2(o4.x, o4.y);
+      float r[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) r[i] = oscale(acc[i]);
+      const float g0 = lane_xor1(c ? r[0] : r[2]), g1 = lane_xor1(c ? r[1] : r[3]);
+      const float4 o4 = c ? make_float4(g0, r[2], g1, r[3]) : make_float4(r[0], g0, r[1], g1);
+      const int64_t k = k_t + cbase + 16u * (uint32_t)b + 4u * (uint32_t)q + 2u * (uint32_t)c;
+      if (k >= 0 && (uint64_t)k + 1 < p.N) {
+        if constexpr (OA) {
+          store16_nt(reinterpret_cast<float4*>(out + k), o4);
+        } else {
+          out[k] = make_float2(o4.x, o4.y);
+          out[k + 1] = make_float2(o4.z, o4.w);
+        }
+      } else {
+        if (k >= 0 && (uint64_t)k < p.N) out[k] = make_float2(o4.x, o4.y);
+        if (k + 1 >= 0 && (uint64_t)(k + 1) < p.N) out[k + 1] = make_float2(o4.z, o4.w);
       }
     }
     __syncthreads();  // every wave is done reading the tile's planes
   }
 }
-
-
 
 // ------------------------------------------------------------------------------------------------
 // int8 I/Q FM / AM chains on the matrix cores (gsdrxFmDemodInt8 / gsdrxAmDemodInt8, D = 4, T <= 132).
@@ -199,27 +356,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
 //   y[k] = sum_i t_i x[4k+i] e^{j phi(4k+i)} = e^{j phi(4k)} y'[k],  y'[k] = sum_i t'_i x[4k+i],
 //   t'_i = t_i e^{j 2 pi (i inc mod 2^32) / 2^32}
 // (the phase is additive mod 2^32). The AM envelope |y| = |y'|, and the FM discriminator
-// arg(y[k+1] conj y[k]) = arg(y'[k+1] conj y'[k]) + 2 pi (4 inc mod 2^32) / 2^32 (wrapped), so neither
-// needs the rotation: the chain is a complex-tap FIR on the raw int8 samples, exact in fp16 as in
-// k_fir_i8_mfma. Complex taps on real planes: with P/Q' the real/imaginary-tap sums of the I column and
-// R/S those of the Q column, y' = (P - S) + j (R + Q'); two fp16 parts per tap component -> 4 MFMAs per
-// 32-sample step. FM tiles overlap by one output (stride KT - 1) and stage 8-byte granules, so every
-// tile start stays aligned. Normwise parity with the float chains, not bit identity (gsdr_ext.h).
+// arg(y[k+1] conj y[k]) = arg(y'[k+1] conj y'[k]) + 2 pi (4 inc mod 2^32) / 2^32 (wrapped) wherever that
+// product is nonzero, so neither needs the rotation: the chain is a complex-tap FIR on the raw int8
+// samples, with the taps split into three exact bf16 parts as in k_fir_i8_mfma.
+// Layout: a C tile is 64 consecutive outputs. A's rows 0-7 hold the real parts t'r of 8 consecutive
+// outputs' taps and rows 8-15 the imaginary parts t'i of the same 8 outputs (A[m][kk] = t'r[kk - 4m],
+// A[8 + m][kk] = t'i[kk - 4m]); column n = 2 b + c is component c of the 8-output block b. So one MFMA
+// gives both tap sums, K = 7 D + T = 155 fits 5 steps (a 16-output row block needs 6 and twice the
+// registers), and per 32-sample step 3 MFMAs (one a part). With P / Q' the real / imaginary-tap sums of
+// the I column and R / S those of the Q column, y' = (P - S) + j (R + Q'): lane (q, n) and lane
+// (q ^ 2, n ^ 1) hold the two terms of one component, one lane exchange apart.
+// FM tiles overlap by 16 outputs (stride KT - 16, so every tile start stays a 16-multiple of the absolute
+// output index); the tile's y' go through LDS to the discriminator pass (coalesced 4-byte stores).
+// Normwise parity with the float chains, not bit identity (gsdr_ext.h).
 // ------------------------------------------------------------------------------------------------
 template <int MODE, int NCT_ = 4>
 struct I8ChainMfma {
   static constexpr int D = 4;
   static constexpr int WG = 256;
-  static constexpr int NCT = NCT_;
-  static constexpr int KT = (WG / 64) * NCT * 128;
-  static constexpr int STRIDE = MODE == kModeFm ? KT - 1 : KT;
-  static constexpr int MAXNS = 6;
-  static constexpr int MAXT = 32 * MAXNS - 15 * D;  // 132
-  static constexpr int SPAN = (KT - 16) * D + 32 * MAXNS;
-  static constexpr int NG = SPAN / 4;  // 8-byte granules (4 samples)
-  static constexpr int NGR = (NG + WG - 1) / WG;
+  static constexpr int NCT = NCT_;                 // C tiles (64 outputs) per wave and tile
+  static constexpr int KT = (WG / 64) * NCT * 64;  // y' per tile (a multiple of 16)
+  static constexpr int STRIDE = MODE == kModeFm ? KT - 16 : KT;
+  static constexpr int MAXNS = 5;
+  static constexpr int MAXT = 32 * MAXNS - 7 * D;  // 132
+  static constexpr int SPAN = (KT - 8) * D + 32 * MAXNS;
   static_assert(SPAN % 4 == 0, "whole granules");
-  __host__ __device__ static constexpr uint32_t addr(uint32_t idx) { return idx * 2u + (idx / 64u) * 16u; }
+  __host__ __device__ static constexpr uint32_t addr(uint32_t idx) { return i8_addr(idx); }
   static constexpr uint32_t PLANE = (addr(SPAN) + 255u) / 256u * 256u + 128u;
   static constexpr uint32_t LDS_BYTES = PLANE + addr(SPAN);
 };
@@ -229,45 +391,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
   using C = I8ChainMfma<MODE, NCT>;
   constexpr int D = C::D;
   __shared__ __attribute__((aligned(16))) char lds[C::LDS_BYTES];
-  __shared__ float4 ybuf[MODE == kModeFm ? C::KT / 2 : 1];  // FM: the tile's FIR outputs y'
+  __shared__ float2 ybuf[MODE == kModeFm ? C::KT : 1];  // FM: the tile's FIR outputs y'
   __shared__ float wmax[C::WG / 64];
   __shared__ uint32_t wbad[C::WG / 64];
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
   const float* __restrict__ taps = reinterpret_cast<const float*>(p.taps);
   const Iq8* __restrict__ in = reinterpret_cast<const Iq8*>(p.in);
   float* __restrict__ out = reinterpret_cast<float*>(p.out);
   const uint32_t T = p.T;
+  const int64_t phase = (int64_t)p.out_phase;
 
   // modulated taps t'_i = t_i e^{j 2 pi (i inc) / 2^32}
   const float t = tid < T ? taps[tid] : 0.0f;
   const float2 ph = nco_direct(tid * p.nco_inc);
   const float tr = t * ph.x, ti = t * ph.y;
-  float a = fmaxf(fabsf(tr), fabsf(ti));
+  float amax = fmaxf(fabsf(tr), fabsf(ti));
   uint32_t bad = isfinite(t) ? 0u : 1u;
-  for (int o = 32; o > 0; o >>= 1) {
-    a = fmaxf(a, __shfl_xor(a, o, 64));
-    bad |= __shfl_xor(bad, o, 64);
+  wg_max_bad<C::WG>(amax, bad, wmax, wbad);
+  const int sc = i8_tap_scale(amax);
+  if (!bad) {
+    __bf16 b1, b2, b3;
+    uint32_t inexact = (split3(ldexpf(tr, sc), b1, b2, b3) && split3(ldexpf(ti, sc), b1, b2, b3)) ? 0u : 1u;
+    float dummy = 0.0f;
+    __syncthreads();
+    wg_max_bad<C::WG>(dummy, inexact, wmax, wbad);
+    bad = inexact;
   }
-  if (lane == 0) {
-    wmax[w] = a;
-    wbad[w] = bad;
-  }
-  __syncthreads();
-  float amax = wmax[0];
-  bad = wbad[0];
-#pragma unroll
-  for (int i = 1; i < C::WG / 64; ++i) {
-    amax = fmaxf(amax, wmax[i]);
-    bad |= wbad[i];
-  }
-  if (bad) {  // non-finite taps: the exact per-output chain (the generic kernel's evaluation)
+  if (bad) {  // non-finite or unsplittable taps: the exact per-output chain (the generic kernel's evaluation)
     for (uint32_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
       for (uint32_t r = tid; r < (uint32_t)C::STRIDE; r += C::WG) {
-        const uint64_t k = (uint64_t)tile * C::STRIDE + r;
-        if (k >= p.N) continue;
-        const float2 y0 = fir_point<float, Iq8, MODE>(p, k);
+        const int64_t k = (int64_t)tile * C::STRIDE - phase + r;
+        if (k < 0 || (uint64_t)k >= p.N) continue;
+        const float2 y0 = fir_point<float, Iq8, MODE>(p, (uint64_t)k);
         if constexpr (MODE == kModeFm) {
-          out[k] = fm_disc(y0, fir_point<float, Iq8, MODE>(p, k + 1), p.fm_gain);
+          out[k] = fm_disc(y0, fir_point<float, Iq8, MODE>(p, (uint64_t)k + 1), p.fm_gain);
         } else {
           out[k] = am_env(y0);
         }
@@ -275,141 +432,129 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
     }
     return;
   }
-  int e = 0;
-  (void)frexpf(amax, &e);
-  const int sc = 14 - e;
   float* ldsT = reinterpret_cast<float*>(lds);
   ldsT[tid] = ldexpf(tr, sc);
   ldsT[C::WG + tid] = ldexpf(ti, sc);
   __syncthreads();
-  gsdr_h8 arh[C::MAXNS], arl[C::MAXNS], aih[C::MAXNS], ail[C::MAXNS];
+  gsdr_b8 a1[C::MAXNS], a2[C::MAXNS], a3[C::MAXNS];
   {
-    const int m = (int)(lane & 15u), q = (int)(lane >> 4);
+    const int m = (int)(lane & 7u), im = (int)((lane >> 3) & 1u), q = (int)(lane >> 4);
+    const float* tab = ldsT + (im ? C::WG : 0);
 #pragma unroll
     for (int s = 0; s < C::MAXNS; ++s) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int i = 32 * s + 8 * q + j - D * m;  // <= 191 < WG
-        const float vr = i >= 0 ? ldsT[i] : 0.0f, vi = i >= 0 ? ldsT[C::WG + i] : 0.0f;
-        const _Float16 hr = (_Float16)vr, hi = (_Float16)vi;
-        arh[s][j] = hr;
-        arl[s][j] = (_Float16)(vr - (float)hr);
-        aih[s][j] = hi;
-        ail[s][j] = (_Float16)(vi - (float)hi);
+        const int i = 32 * s + 8 * q + j - D * m;  // <= 159 < WG
+        __bf16 b1, b2, b3;
+        (void)split3(i >= 0 ? tab[i] : 0.0f, b1, b2, b3);
+        a1[s][j] = b1;
+        a2[s][j] = b2;
+        a3[s][j] = b3;
       }
     }
   }
-  const float oscale = ldexpf(1.0f / 127.0f, -sc);
   // FM: the rotation the taps leave out, 2 pi (4 inc mod 2^32) / 2^32 in (-pi, pi]
   const float dphi = (float)((double)(int32_t)(4u * p.nco_inc) * (6.283185307179586 / 4294967296.0));
+  const I8OutScale oscale(sc);
   __syncthreads();
 
-  const int n = (int)(lane & 15u), q = (int)(lane >> 4), c = n & 1, b = n >> 1;
+  const uint32_t n = lane & 15u, q = lane >> 4, c = n & 1u, b = n >> 1;
+  const uint32_t hi = q >> 1;         // rows 8-15 (imaginary-tap sums)
+  const bool is_re = (c == 0) == (hi == 0);  // this lane ends up with Re y' (else Im y')
+  // one output a lane: lanes (q, c) of a block pair up as (Re, Im) of rows 4 (q & 1) + sel
+  const uint32_t sel = 2u * hi + (is_re ? 0u : 1u);
+  const bool sel_b0 = !is_re;  // the partner lane keeps row sel ^ 1
+  const uint32_t hmask = hi ? 0xffffffffu : 0u, b0mask = sel_b0 ? 0xffffffffu : 0u;
+  // sign flips for Re = P - S: the P lane (q < 2) negates the partner's S, the S lane (q >= 2) its own
+  const uint32_t sg_acc = (is_re && hi) ? 0x80000000u : 0u, sg_oth = (is_re && !hi) ? 0x80000000u : 0u;
   const char* bplane = lds + (c ? C::PLANE : 0u);
+  const uint32_t w = tid >> 6;
+  I8Stage<4, C::SPAN, C::WG> st;
+  if (blockIdx.x < tiles) i8_load_granules<4, VEC>(st, in, ((int64_t)blockIdx.x * C::STRIDE - phase) * D, p.L);
   for (uint32_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
-    const uint64_t k_t = (uint64_t)tile * C::STRIDE;
-    const uint64_t S0 = k_t * D;
-    uint2 wv[C::NGR];
-#pragma unroll
-    for (int r = 0; r < C::NGR; ++r) {
-      const uint32_t g = tid + (uint32_t)r * C::WG;
-      const uint64_t s = S0 + 4ull * g;
-      wv[r] = make_uint2(0u, 0u);
-      if (g < (uint32_t)C::NG) {
-        if (VEC && s + 4 <= p.L) {
-          typedef uint32_t u2v __attribute__((ext_vector_type(2)));
-          const u2v t2 = __builtin_nontemporal_load(reinterpret_cast<const u2v*>(in + s));
-          wv[r] = make_uint2(t2.x, t2.y);
-        } else {
-          uint32_t d[2];
-#pragma unroll
-          for (int k = 0; k < 2; ++k) {
-            const Iq8 a0 = s + 2 * k < p.L ? in[s + 2 * k] : Iq8{0, 0};
-            const Iq8 a1 = s + 2 * k + 1 < p.L ? in[s + 2 * k + 1] : Iq8{0, 0};
-            d[k] = (uint32_t)(uint8_t)a0.x | (uint32_t)(uint8_t)a0.y << 8 | (uint32_t)(uint8_t)a1.x << 16 |
-                   (uint32_t)(uint8_t)a1.y << 24;
-          }
-          wv[r] = make_uint2(d[0], d[1]);
-        }
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < C::NGR; ++r) {
-      const uint32_t g = tid + (uint32_t)r * C::WG;
-      if (g < (uint32_t)C::NG) {
-        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-        h4 hi_, hq_;
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-          const uint32_t wd = k ? wv[r].y : wv[r].x;
-#pragma unroll
-          for (int u = 0; u < 2; ++u) {  // gsdrInt8ToNormFloat clamps -128 to -1.0 = -127 / 127
-            hi_[2 * k + u] = (_Float16)max((int)(wd << (24 - 16 * u)) >> 24, -127);
-            hq_[2 * k + u] = (_Float16)max((int)(wd << (16 - 16 * u)) >> 24, -127);
-          }
-        }
-        const uint32_t o = C::addr(4u * g);
-        *reinterpret_cast<h4*>(lds + o) = hi_;
-        *reinterpret_cast<h4*>(lds + C::PLANE + o) = hq_;
-      }
-    }
+    const int64_t k_t = (int64_t)tile * C::STRIDE - phase;  // a multiple of 16 in absolute output index
+    i8_store_planes(st, lds, C::PLANE);
     __syncthreads();
-    float4 res[C::NCT];
+    // the next tile's loads fly while this one is computed
+    if (tile + gridDim.x < tiles) i8_load_granules<4, VEC>(st, in, (k_t + (int64_t)gridDim.x * C::STRIDE) * D, p.L);
 #pragma unroll
     for (int ct = 0; ct < C::NCT; ++ct) {
-      const uint32_t cbase = (w * C::NCT + (uint32_t)ct) * 128u;
-      const uint32_t idx0 = (cbase + 16u * (uint32_t)b) * D + 8u * (uint32_t)q;
-      gsdr_f4v ar = {0.0f, 0.0f, 0.0f, 0.0f}, ai = ar;
+      const uint32_t cbase = (w * C::NCT + (uint32_t)ct) * 64u;
+      const uint32_t idx0 = (cbase + 8u * b) * D + 8u * q;
+      gsdr_f4v acc = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-      for (int s = 0; s < C::MAXNS; ++s) {
-        if ((uint32_t)s < ns) {
-          const gsdr_h8 bf = *reinterpret_cast<const gsdr_h8*>(bplane + C::addr(idx0 + 32u * (uint32_t)s));
-          ar = __builtin_amdgcn_mfma_f32_16x16x32_f16(arl[s], bf, ar, 0, 0, 0);
-          ai = __builtin_amdgcn_mfma_f32_16x16x32_f16(ail[s], bf, ai, 0, 0, 0);
-          ar = __builtin_amdgcn_mfma_f32_16x16x32_f16(arh[s], bf, ar, 0, 0, 0);
-          ai = __builtin_amdgcn_mfma_f32_16x16x32_f16(aih[s], bf, ai, 0, 0, 0);
-        }
+      for (int s = 0; s < C::MAXNS; ++s) {  // steps past 15 D + T meet zero taps
+        const gsdr_b8 bf = *reinterpret_cast<const gsdr_b8*>(bplane + C::addr(idx0 + 32u * (uint32_t)s));
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a3[s], bf, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2[s], bf, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[s], bf, acc, 0, 0, 0);
       }
-      // I lane (c = 0): ar = P, ai = Q'; Q lane: ar = R, ai = S.  y' = (P - S) + j (R + Q')
-      float v[4];
+      // lane (q, c) holds rows 4q .. 4q + 3 of column (b, c): P (q < 2, c = 0), R (q < 2, c = 1),
+      // Q' (q >= 2, c = 0), S (q >= 2, c = 1); its partner lane ^ 33 holds the other term of one component
+      // This lane needs rows 2 hi and 2 hi + 1 of its component (the rows it and its lane ^ 1 partner keep);
+      // lane ^ 33 needs the other two: swap them, then Re = P - S, Im = R + Q' (commutative), as
+      // (+-acc) + (+-other) with per-lane signs, the same rounded operation on both lanes of a pair
+      float v[2];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float other = __shfl_xor(ai[i], 1, 64);
-        v[i] = (c ? ar[i] + other : ar[i] - other) * oscale;
+      for (int j = 0; j < 2; ++j) {
+        // bit selects (v_bfi_b32) with a lane mask, not a runtime index into acc (which compiles to compare chains)
+        const uint32_t lo_ = __float_as_uint(acc[j]), hi_ = __float_as_uint(acc[2 + j]);
+        const float keep = __uint_as_float((hi_ & hmask) | (lo_ & ~hmask));
+        const float give = __uint_as_float((lo_ & hmask) | (hi_ & ~hmask));
+        const float other = lane_xor1(lane_xor32(give));
+        const float pa = __int_as_float(__float_as_int(keep) ^ sg_acc);
+        const float po = __int_as_float(__float_as_int(other) ^ sg_oth);
+        v[j] = oscale(pa + po);
       }
-      // lane (q, b, c) keeps rows 2c, 2c + 1 of its 4q group, both components
-      const float g0 = __shfl_xor(c ? v[0] : v[2], 1, 64), g1 = __shfl_xor(c ? v[1] : v[3], 1, 64);
-      res[ct] = c ? make_float4(g0, v[2], g1, v[3]) : make_float4(v[0], g0, v[1], g1);
+      // the Re and Im lanes of these two rows are lane and lane ^ 1; lane keeps row sel, sends row sel ^ 1
+      const uint32_t v0 = __float_as_uint(v[0]), v1 = __float_as_uint(v[1]);
+      const float mine = __uint_as_float((v1 & b0mask) | (v0 & ~b0mask));
+      const float got = lane_xor1(__uint_as_float((v0 & b0mask) | (v1 & ~b0mask)));
+      // (Re, Im): the Re lane's own value first (b0mask is all ones exactly on the Im lanes)
+      const uint32_t mi = __float_as_uint(mine), gi = __float_as_uint(got);
+      const float2 y = make_float2(__uint_as_float((gi & b0mask) | (mi & ~b0mask)),
+                                   __uint_as_float((mi & b0mask) | (gi & ~b0mask)));
+      const uint32_t rr = cbase + 8u * b + 4u * (q & 1u) + sel;  // this lane's output within the tile
       if constexpr (MODE == kModeAm) {
-        const uint32_t rr = cbase + 16u * (uint32_t)b + 4u * (uint32_t)q + 2u * (uint32_t)c;
-        const uint64_t k = k_t + rr;
-        const float e0 = am_env(make_float2(res[ct].x, res[ct].y)), e1 = am_env(make_float2(res[ct].z, res[ct].w));
-        if (k + 1 < p.N) {
-          *reinterpret_cast<float2*>(out + k) = make_float2(e0, e1);
-        } else if (k < p.N) {
-          out[k] = e0;
-        }
+        const int64_t k = k_t + rr;
+        if (k >= 0 && (uint64_t)k < p.N) out[k] = am_env(y);
+      } else {
+        ybuf[rr] = y;
       }
     }
     if constexpr (MODE == kModeFm) {
-      // the tile's y' in their own LDS slots (y'[rr], y'[rr + 1] at float4 slot rr / 2), then one barrier
-      // for both the planes (read by every wave's MFMAs) and y' (read across waves below); the next
-      // tile's staging barrier orders this pass's reads before the next writes of ybuf
-#pragma unroll
-      for (int ct = 0; ct < C::NCT; ++ct) {
-        const uint32_t rr = (w * C::NCT + (uint32_t)ct) * 128u + 16u * (uint32_t)b + 4u * (uint32_t)q + 2u * (uint32_t)c;
-        ybuf[rr >> 1] = res[ct];
-      }
+      // one barrier for both the planes (read by every wave's MFMAs) and y' (read across waves below); the
+      // next tile's staging barrier orders this pass's reads before the next writes of ybuf
       __syncthreads();
-      const float2* y2 = reinterpret_cast<const float2*>(ybuf);
-      for (uint32_t r = tid; r < (uint32_t)C::STRIDE; r += C::WG) {
-        const uint64_t k = k_t + r;
-        if (k < p.N) {
-          const float2 z = disc_product(y2[r], y2[r + 1]);
-          float ang = disc_atan2(z.y, z.x) + dphi;
-          ang = ang > 3.14159274f ? ang - 6.28318548f : (ang <= -3.14159274f ? ang + 6.28318548f : ang);
-          out[k] = p.fm_gain * ang;
+      // two outputs a thread and step on packed FMAs (disc_angle2); r1 = r0 + WG
+      for (uint32_t r0 = tid; r0 < (uint32_t)C::STRIDE; r0 += 2u * C::WG) {
+        const uint32_t r1 = r0 + C::WG < (uint32_t)C::STRIDE ? r0 + C::WG : r0;
+        const float2 za = disc_product(ybuf[r0], ybuf[r0 + 1]), zb = disc_product(ybuf[r1], ybuf[r1 + 1]);
+        const gsdr_f32x2 a2 = disc_angle2(za, zb) + gsdr_f32x2{dphi, dphi};
+        float ang[2] = {a2.x, a2.y};
+        const float2 zz[2] = {za, zb};
+        const uint32_t rr[2] = {r0, r1};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          ang[h] = ang[h] > 3.14159274f ? ang[h] - 6.28318548f : (ang[h] <= -3.14159274f ? ang[h] + 6.28318548f : ang[h]);
+          if (zz[h].x == 0.0f && zz[h].y == 0.0f) {
+            // arg(y[k+1] conj y[k]) = arg(z') + dphi needs z' != 0. An exactly zero product (a zero window
+            // beside a nonzero one, silence, zero taps) gives the reference's atan2f(+-0, +-0) (fm.cu:66-68),
+            // whose value (0 or +-pi) follows the signs of the ROTATED outputs y = e^{j phi(4k)} y': rotate
+            // the nonzero ones; a zero window's y is +0 + j0 in the reference's ascending sum from +0
+            const float2 y0 = ybuf[rr[h]], y1 = ybuf[rr[h] + 1];
+            const uint32_t n = p.nco_n0 + 4u * (uint32_t)(k_t + rr[h]);
+            const float2 u0 = (y0.x == 0.0f && y0.y == 0.0f) ? make_float2(0.0f, 0.0f)
+                                                             : cmul(y0, nco_direct(n * p.nco_inc));
+            const float2 u1 = (y1.x == 0.0f && y1.y == 0.0f) ? make_float2(0.0f, 0.0f)
+                                                             : cmul(y1, nco_direct((n + 4u) * p.nco_inc));
+            const float2 zr = disc_product(u0, u1);
+            ang[h] = atan2f(zr.y, zr.x);
+          }
         }
+        const int64_t k0 = k_t + r0, k1 = k_t + r1;
+        if (k0 >= 0 && (uint64_t)k0 < p.N) out[k0] = p.fm_gain * ang[0];
+        if (r1 != r0 && k1 >= 0 && (uint64_t)k1 < p.N) out[k1] = p.fm_gain * ang[1];
       }
     } else {
       __syncthreads();  // every wave is done reading the tile's planes

@@ -49,6 +49,9 @@ static hipError_t chain_entry(int mode, float fs, float tune, float chan, float 
   job.mode = mode;
   job.variant = variant;
   job.nco_n0 = (uint32_t)firstSampleIndex;
+  // the int8 matrix-core chains align their 16-output blocks to the absolute output index
+  // firstSampleIndex / D + k, so chunked calls reproduce one call bit for bit (fir_i8_mfma.hpp)
+  job.out_phase = (uint32_t)((firstSampleIndex / decimation) & 15u);
   if (mode == kModeFm) {
     job.L = numOutputs * (size_t)decimation + tapCount;  // N + 1 FIR outputs
     job.fm_gain = fs / (2.0f * kPiF * dev);              // as reference src/fm.cu:203
@@ -85,7 +88,13 @@ static hipError_t chain_multi_entry(int mode, float fs, float tune, const float*
     }
     float* out = output + (size_t)c0 * numOutputs;
     hipError_t e = hipErrorNotSupported;
-    if (tapCount > 0) {
+    // int8 I/Q at decimation 4: the single-channel default is the matrix-core chain, so each channel runs
+    // it (bit-identical to gsdrxFmDemodInt8 / gsdrxAmDemodInt8 with that channel's frequency)
+    bool grouped = tapCount > 0;
+    if constexpr (std::is_same<InT, Iq8>::value) {
+      if (decimation == 4 && tapCount <= (size_t)I8ChainMfma<kModeFm>::MAXT) grouped = false;
+    }
+    if (grouped) {
       FirJob job;
       job.in = input;
       job.taps = taps;
@@ -158,17 +167,6 @@ GSDR_C_LINKAGE hipError_t gsdrxAmDemodInt8(float rfSampleRate, float tuningFrequ
                            output, numElements, cudaDevice, cudaStream);
 }
 
-namespace gsdr {
-// int8 FM / AM chain on the exact packed-VALU path (bit-identical to gsdrInt8ToNormFloat + the float chain):
-// the streaming object's int8 chains, whose chunked output must reproduce one call bit for bit (the
-// decimation-4 matrix-core default sums in an order that depends on where a call starts)
-hipError_t chain_int8_exact(int mode, float fs, float tune, float chan, float dev, uint32_t decimation,
-                            size_t firstSampleIndex, const float* taps, size_t tapCount, const int8_t* input,
-                            float* output, size_t numOutputs, int32_t device, hipStream_t stream) {
-  return chain_entry(mode, fs, tune, chan, mode == kModeFm ? dev : 1.0f, decimation, firstSampleIndex, taps, tapCount,
-                     reinterpret_cast<const Iq8*>(input), output, numOutputs, device, stream, 0);
-}
-}  // namespace gsdr
 
 GSDR_C_LINKAGE uint32_t gsdrNcoPhaseIncrement(float rfSampleRate, float tuningFrequency,
                                               float channelFrequency) GSDR_NO_EXCEPT {

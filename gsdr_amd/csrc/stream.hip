@@ -40,12 +40,10 @@ struct gsdrxStream_t {
 };
 
 namespace gsdr {
-// fm_am.hip: the int8 chains on the exact path (kModeFm = 1, kModeAm = 2 as in fir_engine.hpp)
-hipError_t chain_int8_exact(int mode, float fs, float tune, float chan, float dev, uint32_t decimation,
-                            size_t firstSampleIndex, const float* taps, size_t tapCount, const int8_t* input,
-                            float* output, size_t numOutputs, int32_t device, hipStream_t stream);
-
-constexpr int kChainFm = 1, kChainAm = 2;
+// fir_int8.hip: gsdrxFirFCInt8 for outputs starting at absolute output index outputIndex
+hipError_t fir_int8_at(uint64_t outputIndex, size_t decimation, const float* taps, size_t tapCount,
+                       const int8_t* input, hipFloatComplex* output, size_t numOutputs, int32_t device,
+                       hipStream_t stream);
 
 namespace {
 
@@ -74,20 +72,19 @@ hipError_t filter(const gsdrxStream_t& s, const void* in, uint64_t first, void* 
   const bool i8 = s.format == GSDRX_SAMPLES_CS8;
   switch (s.kind) {
     case GSDRX_STREAM_FIR:
-      // variant 0: the exact packed-VALU path for every decimation. The matrix-core default of
-      // gsdrxFirFCInt8 (D = 4) sums in an order that depends on an output's position within its 16-output
-      // block, i.e. on where a call starts, so chunked calls could not reproduce one monolithic call.
-      return i8 ? gsdrxFirFCInt8Variant(0, s.D, s.taps, s.T, static_cast<const int8_t*>(in),
-                                        static_cast<hipFloatComplex*>(out), n, s.device, st)
+      // the default path of gsdrxFirFCInt8 told the output's absolute index: the decimation-4 matrix-core
+      // kernel aligns its summation blocks to it, so chunks reproduce one call (fir_i8_mfma.hpp)
+      return i8 ? fir_int8_at((first - s.n0) / s.D, s.D, s.taps, s.T, static_cast<const int8_t*>(in),
+                              static_cast<hipFloatComplex*>(out), n, s.device, st)
                 : gsdrFirFC(s.D, s.taps, s.T, static_cast<const hipFloatComplex*>(in),
                             static_cast<hipFloatComplex*>(out), n, s.device, st);
     case GSDRX_STREAM_FM:
-      return i8 ? chain_int8_exact(kChainFm, s.fs, s.tune, s.chan, s.dev, s.D, first, s.taps, s.T,
+      return i8 ? gsdrxFmDemodInt8(s.fs, s.tune, s.chan, s.dev, s.D, first, s.taps, s.T,
                                    static_cast<const int8_t*>(in), static_cast<float*>(out), n, s.device, st)
                 : gsdrFmDemod(s.fs, s.tune, s.chan, s.dev, s.D, first, s.taps, s.T,
                               static_cast<const hipFloatComplex*>(in), static_cast<float*>(out), n, s.device, st);
     default:
-      return i8 ? chain_int8_exact(kChainAm, s.fs, s.tune, s.chan, 1.0f, s.D, first, s.taps, s.T,
+      return i8 ? gsdrxAmDemodInt8(s.fs, s.tune, s.chan, s.D, first, s.taps, s.T,
                                    static_cast<const int8_t*>(in), static_cast<float*>(out), n, s.device, st)
                 : gsdrAmDemod(s.fs, s.tune, s.chan, s.D, first, s.taps, s.T, static_cast<const hipFloatComplex*>(in),
                               static_cast<float*>(out), n, s.device, st);

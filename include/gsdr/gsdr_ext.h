@@ -60,12 +60,18 @@ GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxFirFCVariant(
 
 /**
  * gsdrFirFC (fir.h) on int8 I/Q input.
- * Exception to the bit-identity above: decimation 4 with tapCount <= 196 and a 16-byte aligned output
- * runs on the matrix cores (samples exact in fp16, taps scaled by a power of two and split into two
- * fp16 parts, fp32 accumulation in the matrix core's order), which meets the floating-point parity bar
- * of the float path -- max_k |y - y_float| / sum_i |t_i||x_(4k+i)| <= 1e-5 -- rather than matching it
- * bit for bit; taps that are not all finite take the exact ascending loop. Variant 0 of
- * gsdrxFirFCInt8Variant is the bit-identical packed-VALU path.
+ * Exception to the bit-identity above: decimation 4 with tapCount <= 196 runs on the matrix cores. The
+ * samples are exact in bf16; the taps are scaled by a power of two and split EXACTLY into three bf16
+ * parts (t = b1 + b2 + b3, 8 significant bits each, fp32's exponent range), so every product is exact and
+ * the only roundings are the fp32 accumulation, in the matrix core's order, and the final scale. For every
+ * input -- dense, sparse or impulsive, with taps spanning any range a float holds -- the result meets the
+ * floating-point parity bar of the float path, max_k |y_k - y_float,k| / sum_i |t_i||x_(4k+i)| <= 1e-5
+ * (an output whose window is all zero is exactly zero), rather than matching it bit for bit. Taps that are
+ * not all finite, or whose nonzero magnitudes span more than ~2^200 (no exact split), take the exact
+ * ascending loop. The summation order of output k depends only on the taps, its own window and
+ * k mod 16 (k counted from the first output of the call; the streaming object, stream.h, passes the
+ * stream's absolute output index instead), so the bits do not depend on the input or output pointers'
+ * alignment. Variant 0 of gsdrxFirFCInt8Variant is the bit-identical packed-VALU path.
  */
 GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxFirFCInt8(
     size_t decimation,
@@ -94,9 +100,20 @@ GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxFirFCInt8Variant(
  * gsdrFmDemod (fm.h) on int8 I/Q input. Exception to the bit-identity above: decimation 4 with
  * numLowPassTaps <= 132 runs on the matrix cores with the NCO folded into complex taps
  * t_i e^{j 2 pi (i inc mod 2^32) / 2^32} (the discriminator adds the 4-sample phase step back, the
- * envelope needs no rotation), samples exact in fp16, taps in two fp16 parts: the float chain's parity
- * bar (wrapped angle within 1e-5 pi g of it) rather than its bits; non-finite taps take the exact
- * per-output chain. The streaming object's int8 chains (stream.h) keep the exact path.
+ * envelope needs no rotation), samples exact in bf16 and the complex taps split exactly into three bf16
+ * parts as in gsdrxFirFCInt8. Parity with the float chain, not its bits:
+ *   - the FIR outputs y meet the normwise bar above, so the envelope is within 1e-5 of the float chain's
+ *     wherever |x| <= 1 (the int8 range);
+ *   - the discriminator angle follows y: on a constant-envelope (FM) signal it is within 1e-5 pi g of the
+ *     float chain's; an output whose window cancels to a small |y| (noise only, an out-of-band channel) or
+ *     whose product y[k+1] conj y[k] falls below fp32's normal range is as uncertain as any fp32 evaluation
+ *     of it (tests/helpers.py fm_conditioned_err states the bar);
+ *   - where the product is exactly zero (a zero window beside another, silence, zero taps) the output is
+ *     the reference's atan2f(+-0, +-0) value of the rotated outputs (fm.cu:66-68), bit for bit.
+ * Non-finite or unsplittable taps take the exact per-output chain. The summation blocks follow the
+ * absolute output index firstSampleIndex / 4 + k (mod 16), so a stream cut into calls by hand (each call
+ * given its own firstSampleIndex) reproduces one call bit for bit; so do gsdrxStream (stream.h) and
+ * gsdrxFmDemodMulti. A caller that needs gsdrFmDemod's own bits converts with gsdrInt8ToNormFloat first.
  */
 GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxFmDemodInt8(
     float rfSampleRate,
@@ -113,8 +130,8 @@ GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxFmDemodInt8(
     int32_t cudaDevice,
     hipStream_t cudaStream) GSDR_NO_EXCEPT;
 
-/** gsdrAmDemod (am.h) on int8 I/Q input (decimation 4, <= 132 taps, 8-byte aligned output: matrix cores, as
- * gsdrxFmDemodInt8). */
+/** gsdrAmDemod (am.h) on int8 I/Q input (decimation 4, <= 132 taps: the matrix cores, as gsdrxFmDemodInt8;
+ * envelope within 1e-5 of the float chain's). */
 GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxAmDemodInt8(
     float rfSampleRate,
     float tuningFrequency,
@@ -133,11 +150,12 @@ GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxAmDemodInt8(
  * Multi-channel chains (the intent of the reference's unused k_Fm4x,
  * src/fm.cu:71-179): numChannels channels of one RF input, each with its own channel frequency (and
  * FM deviation), sharing the tuning frequency, decimation, taps and firstSampleIndex. Channel c writes
- * output[c * numOutputs + m]; its outputs are bit-identical to gsdrFmDemod / gsdrAmDemod called with
- * channelFrequencies[c] (and frequencyDeviations[c]) -- for int8 I/Q input, on the samples converted by
- * gsdrInt8ToNormFloat (the Int8 variants' exact path; at decimation 4 those run on the matrix cores). For decimation 2, 4
- * and 8 one kernel reads each input tile from HBM once for up to 16 channels; other decimations run
- * the channels one after another. channelFrequencies / frequencyDeviations are host arrays.
+ * output[c * numOutputs + m]; its outputs are bit-identical to gsdrFmDemod / gsdrAmDemod (int8 I/Q input:
+ * gsdrxFmDemodInt8 / gsdrxAmDemodInt8) called with channelFrequencies[c] (and frequencyDeviations[c]).
+ * For decimation 2, 4 and 8 one kernel reads each input tile from HBM once for up to 16 channels; int8
+ * I/Q at decimation 4 with <= 132 taps runs each channel through the single-channel matrix-core chain;
+ * other shapes run the channels one after another. channelFrequencies / frequencyDeviations are host
+ * arrays.
  */
 GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxFmDemodMulti(
     float rfSampleRate,
@@ -176,7 +194,8 @@ GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxAmDemodMulti(
  * Config 5's channel model (BASELINE configs[4]: QPSK256 modulate -> AWGN -> demod): the output of
  * gsdrQpsk256Modulate (the table set by gsdrQpsk256InitConstellation for constellationType) plus
  * additive white Gaussian noise of standard deviation `sigma` per axis, in one pass:
- *     output[k] = table[inputBytes[k]] + (sigma * g0, sigma * g1),  each component rounded once,
+ *     output[k] = table[inputBytes[k]] + (fl(sigma * g0), fl(sigma * g1)),  per component the product
+ *     rounded, then the sum rounded (two roundings, no fused multiply-add),
  * where (g0, g1) are the standard normals of absolute symbol index firstSymbolIndex + k: Box-Muller
  * over Philox4x32-10 keyed by `seed` (the exact construction is in gsdr_amd/csrc/awgn.hpp and its host
  * restatement in oracle/gsdr_oracle.h), built from correctly rounded IEEE operations only. The noise

@@ -19,10 +19,9 @@
  *
  * Kinds: GSDRX_STREAM_FIR (gsdrFirFC), GSDRX_STREAM_FM (gsdrFmDemod), GSDRX_STREAM_AM (gsdrAmDemod).
  * Sample formats: GSDRX_SAMPLES_CF32 (hipFloatComplex) or GSDRX_SAMPLES_CS8 (interleaved int8 I/Q,
- * the gsdrx*Int8 entry points of gsdr_ext.h). An int8 FIR stream runs gsdrxFirFCInt8Variant 0 (the exact
- * path: bit-identical to gsdrInt8ToNormFloat + gsdrFirFC) at every decimation, so it reproduces that
- * call, not the decimation-4 matrix-core default of gsdrxFirFCInt8, whose summation order depends on
- * where a call starts.
+ * the gsdrx*Int8 entry points of gsdr_ext.h). int8 streams reproduce those entry points' defaults, the
+ * decimation-4 matrix-core kernels included: their summation blocks follow the absolute output index
+ * (the stream passes it to every launch), not where a call starts.
  *
  * Threading and streams: one object is one signal stream, and every gsdrxStreamProcess call on it must
  * be given the SAME hipStream_t. The object keeps its history in two device buffers used alternately

@@ -42,3 +42,7 @@ def test_bench_two_ranks_rehearsal(cuda):
     fm = line["secondary"]["fm_chain_multi_gpu"]
     assert fm["n_gpus"] == 2 and fm["us_per_launch_max_over_ranks"] > 0
     assert fm["aggregate_msamples_per_s"] > 0
+    # each rank checked its own channel's output against the float64 restatement, outside the timed region
+    assert fm["parity_ok"] == [True, True], fm
+    assert all(e <= 1e-5 for e in fm["parity_max_wrapped_err_over_pi_g"])
+    assert len(fm["output_digest"]) == 2 and fm["output_digest"][0] != fm["output_digest"][1]  # independent channels

@@ -41,12 +41,11 @@ def test_multi_equals_single(cuda, D, C, int8):
     devs = [2.0e4 + 1000.0 * c for c in range(C)]
     fm = ops.fm_demod_multi(x, taps, FS, TUNE, chans, devs, D, n0, N)
     am = ops.am_demod_multi(x, taps, FS, TUNE, chans, D, n0, N)
-    # int8: the single-channel exact path (conversion + float chain); the D = 4 int8 entry points run
-    # on the matrix cores (normwise, gsdr_ext.h)
-    xs = ops.int8_to_norm_float(x).view(torch.complex64) if int8 else x
+    # int8: the single-channel gsdrx*Int8 defaults (at D = 4 the matrix-core chain, which the multi-channel
+    # entry points then run per channel)
     for c in range(C):
-        f1 = ops.fm_demod(xs, taps, FS, TUNE, chans[c], devs[c], D, n0, N)
-        a1 = ops.am_demod(xs, taps, FS, TUNE, chans[c], D, n0, N)
+        f1 = ops.fm_demod(x, taps, FS, TUNE, chans[c], devs[c], D, n0, N)
+        a1 = ops.am_demod(x, taps, FS, TUNE, chans[c], D, n0, N)
         assert torch.equal(fm[c], f1), c
         assert torch.equal(am[c], a1), c
 

@@ -23,10 +23,8 @@ def chunks(total, seed, W):
 def monolithic(kind, x, taps, D, n0, int8):
     from gsdr_amd import ops
 
-    if int8:
-        # the stream object's int8 kinds run the exact path, bit-identical to conversion + the float
-        # entry point; the D = 4 matrix-core defaults sum in a position-dependent order (stream.h)
-        x = ops.int8_to_norm_float(x).view(torch.complex64)
+    # int8: the gsdrx*Int8 defaults, the decimation-4 matrix-core kernels included (their summation blocks
+    # follow the absolute output index, so the stream's chunk launches reproduce the one call)
     if kind == "fir":
         return ops.fir(taps, x, D)
     if kind == "fm":

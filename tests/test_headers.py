@@ -82,6 +82,6 @@ def test_reference_style_caller_links(tmp_path):
 
 @pytest.mark.skipif(shutil.which("make") is None, reason="needs make")
 def test_example_builds_against_the_library():
-    r = subprocess.run(["make", "-C", ROOT, "examples"], capture_output=True, text=True)
+    r = subprocess.run(["make", "-C", ROOT, "-j8", "examples"], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert os.path.exists(os.path.join(ROOT, "build", "fm_receiver"))

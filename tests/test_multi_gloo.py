@@ -43,7 +43,10 @@ def worker(rank, world, port, q):
         digest = torch.tensor([float(np.abs(y).sum())])
         gathered = [torch.zeros(1) for _ in range(world)]
         dist.all_gather(gathered, digest)  # test-side only: compare the channels the ranks produced
-        q.put((rank, seed, tmax, [float(g) for g in gathered]))
+        # bench's own gather of the per-rank parity flags / digests (fm_multi_gpu)
+        rows = bench.gather_rows(torch, [float(rank == rank), 0.5 * rank, float(10 + rank)], rank, world,
+                                 torch.device("cpu"))
+        q.put((rank, seed, tmax, [float(g) for g in gathered], rows))
     finally:
         dist.destroy_process_group()
 
@@ -66,6 +69,30 @@ def test_two_rank_channels_and_timing():
     assert all(abs(r[2] - 0.020) < 1e-12 for r in results)  # every rank sees the slowest rank's time
     digests = results[0][3]
     assert digests == results[1][3] and digests[0] != digests[1]  # channels really differ
+    for r in results:  # every rank holds every rank's row, in rank order
+        assert r[4] == [[1.0, 0.0, 10.0], [1.0, 0.5, 11.0]]
+
+
+def test_fm_reference_windows_matches_oracle():
+    """bench.fm_reference_windows (the float64 checker of the multi-GPU leg) against the C oracle's FM chain
+    on config 3's signal, on the CPU."""
+    sys.path.insert(0, ROOT)
+    import math
+
+    import bench
+    from gsdr_amd.signals import fm_test_signal, lowpass_taps
+    from oracle import oracle as orc
+
+    T, n, n0 = 127, 3000, 0
+    fs, tune, chan, dev = 1.0e6, 0.0, 1.0e5, 2.0e4
+    x = fm_test_signal(n * 4 + T + 8, noise=0.05, seed=3)
+    taps = lowpass_taps(T, 0.1)
+    refs, g = bench.fm_reference_windows(torch, torch.from_numpy(x), torch.from_numpy(taps), fs, tune, chan, dev, n0,
+                                         [0, 1000, n - 512], 512)
+    want = orc.fm_demod(x, taps, fs, tune, chan, dev, 4, n0, n)
+    for s0, r in zip([0, 1000, n - 512], refs):
+        d = np.remainder(r.numpy() - want[s0:s0 + 512] + math.pi * g, 2 * math.pi * g) - math.pi * g
+        assert np.max(np.abs(d)) / (math.pi * g) <= 2e-6
 
 
 def test_aggregate_is_weak_scaling():

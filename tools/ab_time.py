@@ -6,7 +6,8 @@ clock settle (untimed launches) and then 100 launches inside one HIP event pair.
 per build and workload, and whether outputs equal the first build's bit for bit.
 
     python tools/ab_time.py [other_lib.so ...]     (the in-tree gsdr_amd/libgsdr.so is always first)
-    AB_WORK=fir,fm,fm16  AB_ROUNDS=3   (fm16: gsdrxFmDemodMulti, 16 channels, time per launch)
+    AB_WORK=fir,fm,fm16  AB_ROUNDS=3   (fm16: gsdrxFmDemodMulti, 16 channels, time per launch;
+                                       fir8 / fm8 / am8: the int8 I/Q entry points)
 """
 import ctypes
 import os
@@ -45,6 +46,9 @@ def main():
     xs = [fm_channel(n_in, dev, 100 + k, k * n_in) for k in range(3)]
     x8 = [torch.randint(-128, 128, (2 * n_in,), dtype=torch.int8, device=dev, generator=g) for _ in range(3)] \
         if "fir8" in work else []
+    # config 3's signal quantised to int8 I/Q (the int8 chains)
+    q8 = [torch.clamp(torch.round(torch.view_as_real(x).reshape(-1) * 100), -128, 127).to(torch.int8) for x in xs] \
+        if ("fm8" in work or "am8" in work) else []
     yc = torch.empty(N, dtype=torch.complex64, device=dev)
     yf = torch.empty(N, dtype=torch.float32, device=dev)
     nch = 16
@@ -65,6 +69,12 @@ def main():
                             x.data_ptr(), ym.data_ptr(), N - 1, 0, stream), xs),
         "fir8": ("gsdrxFirFCInt8", [SZ, P, SZ, P, P, SZ, I32, P], yc,
                  lambda x: (D, taps.data_ptr(), T, x.data_ptr(), yc.data_ptr(), N, 0, stream), x8),
+        "fm8": ("gsdrxFmDemodInt8", [F, F, F, F, U32, SZ, P, SZ, P, P, SZ, I32, P], yf,
+                lambda x: (FS, TUNE, CHAN, DEV, D, 0, taps.data_ptr(), T, x.data_ptr(), yf.data_ptr(), N - 1, 0,
+                           stream), q8),
+        "am8": ("gsdrxAmDemodInt8", [F, F, F, U32, SZ, P, SZ, P, P, SZ, I32, P], yf,
+                lambda x: (FS, TUNE, CHAN, D, 0, taps.data_ptr(), T, x.data_ptr(), yf.data_ptr(), N, 0, stream),
+                q8),
     }
     handles = [ctypes.CDLL(p) for p in libs]
     res = {(li, w): [] for li in range(len(libs)) for w in work}

@@ -447,6 +447,7 @@ def secondary_configs(torch, ops, device, taps):
                        "us_per_launch": round(t * 1e6, 2), "msamples_per_s": round(N_IN / t / 1e6, 1),
                        "alg_gbps": round(b / t / 1e9, 1), "alg_bytes_per_launch": b,
                        "fma_tflops": round(4 * TAPS * N_OUT / t / 1e12, 1)}
+    out["fir_int8_stream"] = int8_stream_rate(torch, abi, device, taps, x8s, stream, t)
     del x8s, yf
     # true recursive IIR: 4th-order Butterworth over 2^24 samples
     from scipy import signal as sps
@@ -545,6 +546,51 @@ def secondary_configs(torch, ops, device, taps):
     out["qpsk256"]["demodulate_circular_us"] = round(tc * 1e6, 2)
     out["qpsk256"]["ser_circular_sigma_0.01"] = round(float((rx_bytes != syms).float().mean()), 6)
     return out, c5
+
+
+def int8_stream_rate(torch, abi, device, taps, x8s, stream, t_call, chunks=8):
+    """SURVEY.md 8(f) rows 1 + 2: config 2's int8 channel fed through a gsdrxStream (CS8 FIR, D = 4) in
+    `chunks` equal chunks per pass (seam launches, direct launches and history copies included), passes
+    rotating over the batches, against one gsdrxFirFCInt8 call (t_call) -- the streaming object runs the
+    same matrix-core kernel, its blocks aligned to the stream's output index."""
+    import ctypes
+
+    h = ctypes.c_void_p()
+    rc = abi.lib.gsdrxStreamCreate(ctypes.byref(h), 0, 1, DECIM, taps.data_ptr(), TAPS, 1.0, 0.0, 0.0, 1.0, 0,
+                                   device.index)
+    assert rc == 0, rc
+    cs = N_IN // chunks
+    y = torch.empty(N_OUT + 16, dtype=torch.complex64, device=device)
+    written = ctypes.c_size_t()
+    argsets = []
+    for x in x8s:
+        for c in range(chunks):
+            n = cs if c < chunks - 1 else N_IN - cs * (chunks - 1)
+            argsets.append([x.data_ptr() + 2 * cs * c, n])
+    cnt = [0]
+
+    def one_pass():
+        for _ in range(chunks):
+            p, n = argsets[cnt[0] % len(argsets)]
+            cnt[0] += 1
+            r = abi.lib.gsdrxStreamProcess(h, p, n, y.data_ptr(), y.numel(), ctypes.byref(written), stream)
+            assert r == 0, r
+
+    for _ in range(20):
+        one_pass()
+    torch.cuda.synchronize()
+    reps = 50
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        one_pass()
+    e1.record()
+    torch.cuda.synchronize()
+    t = e0.elapsed_time(e1) / reps * 1e-3
+    abi.lib.gsdrxStreamDestroy(h)
+    return {"config": f"config 2's int8 I/Q channel through gsdrxStream (CS8 FIR, D = 4) in {chunks} chunks a pass",
+            "us_per_channel": round(t * 1e6, 2), "msamples_per_s": round(N_IN / t / 1e6, 1),
+            "vs_single_call": round(t_call / t, 3)}
 
 
 def sq_rule_disagreements(torch, rx, ctype, chunk=1 << 19):

@@ -77,8 +77,9 @@ int main(int argc, char** argv) {
   CHECK(gsdrFmDemod(fs, 0.0f, chan, dev, D, n1 * D, dTaps, T, dX + n1 * D, dFm2 + n1, N - n1, 0, stream));
 
   // extensions: an int8 I/Q front end fed through the streaming object in uneven buffers, which must
-  // reproduce one call of the exact path (gsdrInt8ToNormFloat + gsdrFmDemod) over the whole signal bit for
-  // bit; the one-call gsdrxFmDemodInt8 (decimation 4: matrix cores) meets the float chain's parity bar
+  // reproduce one gsdrxFmDemodInt8 call over the whole signal bit for bit (decimation 4: the matrix-core
+  // chain, whose summation blocks follow the absolute output index); that call meets the float chain's
+  // parity bar against the exact path (gsdrInt8ToNormFloat + gsdrFmDemod)
   std::vector<int8_t> x8(2 * L);
   for (size_t n = 0; n < L; ++n) {
     x8[2 * n] = (int8_t)std::lrint(100.0f * x[n].x);
@@ -126,7 +127,7 @@ int main(int argc, char** argv) {
     return 1;
   }
   // the stream emits every output whose window has arrived: all N (the input holds N*D + T samples)
-  const bool stream_same = produced == N && std::memcmp(fm8.data(), fm8s.data(), N * sizeof(float)) == 0;
+  const bool stream_same = produced == N && std::memcmp(fm8m.data(), fm8s.data(), N * sizeof(float)) == 0;
   // matrix-core int8 chain vs the exact path: wrapped angle within 1e-5 pi g (g = fs / (2 pi dev))
   const double g = fs / (2.0 * 3.141592653589793 * dev);
   double worst = 0.0;

@@ -38,6 +38,13 @@ struct FirJob {
   uint32_t nco_n0 = 0;
   float fm_gain = 0.0f;
   uint32_t out_phase = 0;  // absolute index of output 0 mod 16 (fir_i8_mfma.hpp)
+  // the int8 matrix-core kernels' streaming inputs (FirParams)
+  int64_t in_off = 0;
+  const void* hist = nullptr;
+  uint64_t hist_len = 0;
+  void* hist_out = nullptr;
+  int64_t hist_from = 0;
+  uint64_t hist_n = 0;
 };
 
 // LDS budget per workgroup for the tiled kernels (keeps >= 2 workgroups per CU on 160 KiB).
@@ -56,6 +63,12 @@ inline FirParams make_params(const FirJob& j) {
   p.nco_n0 = j.nco_n0;
   p.fm_gain = j.fm_gain;
   p.out_phase = j.out_phase & 15u;
+  p.in_off = j.in_off;
+  p.hist = j.hist;
+  p.hist_len = j.hist_len;
+  p.hist_out = j.hist_out;
+  p.hist_from = j.hist_from;
+  p.hist_n = j.hist_n;
   return p;
 }
 
@@ -289,8 +302,8 @@ hipError_t launch_i8_mfma_ns(const FirJob& j, hipStream_t s) {
   if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   if (e != hipSuccess) return e;
   const uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)cus * BPC);
-  // tile starts are at sample (j KT - phase) D: byte offset 2 D (j KT - phase) from the input
-  const uintptr_t in0 = reinterpret_cast<uintptr_t>(j.in) - 2u * D * p.out_phase;
+  // tile starts are at sample (j KT - phase) D + in_off: byte offset 2 D (j KT - phase) + 2 in_off
+  const uintptr_t in0 = reinterpret_cast<uintptr_t>(j.in) + (uintptr_t)(2 * j.in_off) - 2u * D * p.out_phase;
   const bool oa = ((reinterpret_cast<uintptr_t>(j.out) - 8u * p.out_phase) % 16) == 0;
 #define GSDR_I8_LAUNCH(G, VEC)                                                                             \
   (oa ? (k_fir_i8_mfma<D, NS, G, VEC, true, BPC><<<dim3(grid), dim3(C::WG), 0, s>>>(p, ns, (uint32_t)tiles), 0) \
@@ -337,8 +350,8 @@ hipError_t launch_chain_i8_mfma(const FirJob& j, hipStream_t s) {
   if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   if (e != hipSuccess) return e;
   const uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)cus * BPC);
-  // tile starts are at sample 4 (j STRIDE - phase): a multiple of 4 samples = 8 bytes from the input
-  if ((reinterpret_cast<uintptr_t>(j.in) % 8) == 0) {
+  // tile starts are at sample 4 (j STRIDE - phase) + in_off: 8 (j STRIDE - phase) + 2 in_off bytes
+  if (((reinterpret_cast<uintptr_t>(j.in) + (uintptr_t)(2 * j.in_off)) % 8) == 0) {
     k_chain_i8_mfma<MODE, true, BPC, NCT><<<dim3(grid), dim3(C::WG), 0, s>>>(p, ns, (uint32_t)tiles);
   } else {
     k_chain_i8_mfma<MODE, false, BPC, NCT><<<dim3(grid), dim3(C::WG), 0, s>>>(p, ns, (uint32_t)tiles);

@@ -191,6 +191,16 @@ struct FirParams {
   uint32_t nco_n0;       // low 32 bits of firstSampleIndex
   float fm_gain;         // FM discriminator gain
   uint32_t out_phase;    // absolute index of output 0 mod 16 (the int8 matrix-core kernels' block grid)
+  // int8 matrix-core kernels only (fir_i8_mfma.hpp; the streaming object's one-launch path): output 0's
+  // window starts at sample in_off of `in`; samples at negative offsets i >= -hist_len come from
+  // hist[hist_len + i] (the stream's history), and samples [hist_from, hist_from + hist_n) (same
+  // offsets) are copied to hist_out (the next history)
+  int64_t in_off;
+  const void* hist;
+  uint64_t hist_len;
+  void* hist_out;
+  int64_t hist_from;
+  uint64_t hist_n;
 };
 
 // ------------------------------------------------------------------------------------------------

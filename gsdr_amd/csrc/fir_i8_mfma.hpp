@@ -70,6 +70,39 @@ __device__ __forceinline__ __bf16 i8_bf16(uint32_t w, int u) {
   return (__bf16)(float)max((int)(w << (24 - 8 * u)) >> 24, -127);
 }
 
+// sample i of the call's input (FirParams::in_off / hist): in[i] for 0 <= i < L, the history before it,
+// zero elsewhere
+__device__ __forceinline__ Iq8 i8_sample(const FirParams& p, int64_t i) {
+  if (i >= 0) return (uint64_t)i < p.L ? reinterpret_cast<const Iq8*>(p.in)[i] : Iq8{0, 0};
+  return (p.hist != nullptr && -i <= (int64_t)p.hist_len) ? reinterpret_cast<const Iq8*>(p.hist)[(int64_t)p.hist_len + i]
+                                                           : Iq8{0, 0};
+}
+
+// The exact per-output evaluation for taps that are not finite or cannot be split: fir_point's ascending
+// loop (fir_engine.hpp), with the samples read through i8_sample (history and offset aware)
+template <int MODE>
+__device__ __forceinline__ float2 i8_point(const FirParams& p, uint64_t k) {
+  const float* __restrict__ taps = reinterpret_cast<const float*>(p.taps);
+  float2 acc;
+  set_zero(acc);
+  const uint64_t s0 = k * p.D;
+  for (uint32_t i = 0; i < p.T; ++i) {
+    auto x = to_lds_sample(i8_sample(p, (int64_t)(s0 + i) + p.in_off));
+    if constexpr (MODE != kModeFir) {
+      x = nco_mix(x, p.nco_n0 + (uint32_t)(s0 + i), p.nco_inc);
+    }
+    mac(acc, x, taps[i]);
+  }
+  return acc;
+}
+
+// The streaming object's next history (FirParams::hist_out), copied by workgroup 0
+__device__ __forceinline__ void i8_copy_history(const FirParams& p) {
+  if (p.hist_out == nullptr || blockIdx.x != 0) return;
+  Iq8* dst = reinterpret_cast<Iq8*>(p.hist_out);
+  for (uint64_t j = threadIdx.x; j < p.hist_n; j += blockDim.x) dst[j] = i8_sample(p, p.hist_from + (int64_t)j);
+}
+
 // Reduce |value| max and a "not exactly representable" flag over the workgroup (WG threads, 64-lane waves).
 template <int WG>
 __device__ __forceinline__ void wg_max_bad(float& a, uint32_t& bad, float* wmax, uint32_t* wbad) {
@@ -134,8 +167,9 @@ struct I8Stage {
 };
 
 template <int G, bool VEC, int SPAN, int WG>
-__device__ __forceinline__ void i8_load_granules(I8Stage<G, SPAN, WG>& st, const Iq8* __restrict__ in, int64_t S0,
-                                                 uint64_t L) {
+__device__ __forceinline__ void i8_load_granules(I8Stage<G, SPAN, WG>& st, const FirParams& p, int64_t S0) {
+  const Iq8* __restrict__ in = reinterpret_cast<const Iq8*>(p.in);
+  const uint64_t L = p.L;
   using S = I8Stage<G, SPAN, WG>;
   const uint32_t tid = threadIdx.x;
   if (VEC && S0 >= 0 && (uint64_t)S0 + SPAN <= L) {
@@ -176,12 +210,10 @@ __device__ __forceinline__ void i8_load_granules(I8Stage<G, SPAN, WG>& st, const
           st.wv[r][0] = t.x;
           st.wv[r][1] = t.y;
         }
-      } else {  // input ends, unaligned input or samples before the buffer: per-sample loads, zero outside
+      } else {  // input ends, unaligned input or samples before the buffer: per-sample loads
 #pragma unroll
         for (int k = 0; k < S::NW; ++k) {
-          const int64_t i0 = s + 2 * k, i1 = i0 + 1;
-          const Iq8 a = (i0 >= 0 && (uint64_t)i0 < L) ? in[i0] : Iq8{0, 0};
-          const Iq8 b = (i1 >= 0 && (uint64_t)i1 < L) ? in[i1] : Iq8{0, 0};
+          const Iq8 a = i8_sample(p, s + 2 * k), b = i8_sample(p, s + 2 * k + 1);
           st.wv[r][k] = (uint32_t)(uint8_t)a.x | (uint32_t)(uint8_t)a.y << 8 | (uint32_t)(uint8_t)b.x << 16 |
                         (uint32_t)(uint8_t)b.y << 24;
         }
@@ -253,10 +285,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
   __shared__ uint32_t wbad[C::WG / 64];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
   const float* __restrict__ taps = reinterpret_cast<const float*>(p.taps);
-  const Iq8* __restrict__ in = reinterpret_cast<const Iq8*>(p.in);
   float2* __restrict__ out = reinterpret_cast<float2*>(p.out);
   const uint32_t T = p.T;
   const int64_t phase = (int64_t)p.out_phase;
+  i8_copy_history(p);
 
   // tap scale (T <= MAXT <= 256: one tap a thread); `bad` = some tap is not finite
   const float t = tid < T ? taps[tid] : 0.0f;
@@ -276,7 +308,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
     for (uint32_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
       for (uint32_t r = tid; r < (uint32_t)C::KT; r += C::WG) {
         const int64_t k = (int64_t)tile * C::KT - phase + r;
-        if (k >= 0 && (uint64_t)k < p.N) out[k] = fir_point<float, Iq8, kModeFir>(p, (uint64_t)k);
+        if (k >= 0 && (uint64_t)k < p.N) out[k] = i8_point<kModeFir>(p, (uint64_t)k);
       }
     }
     return;
@@ -307,13 +339,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
   const int n = (int)(lane & 15u), q = (int)(lane >> 4), c = n & 1, b = n >> 1;
   const char* bplane = lds + (c ? C::PLANE : 0u);
   I8Stage<G, C::SPAN, C::WG> st;
-  if (blockIdx.x < tiles) i8_load_granules<G, VEC>(st, in, ((int64_t)blockIdx.x * C::KT - phase) * D, p.L);
+  if (blockIdx.x < tiles) i8_load_granules<G, VEC>(st, p, ((int64_t)blockIdx.x * C::KT - phase) * D + p.in_off);
   for (uint32_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
     const int64_t k_t = (int64_t)tile * C::KT - phase;  // a multiple of 16 in absolute output index
     i8_store_planes(st, lds, C::PLANE);
     __syncthreads();
     // the next tile's loads fly while this one is computed
-    if (tile + gridDim.x < tiles) i8_load_granules<G, VEC>(st, in, (k_t + (int64_t)gridDim.x * C::KT) * D, p.L);
+    if (tile + gridDim.x < tiles) {
+      i8_load_granules<G, VEC>(st, p, (k_t + (int64_t)gridDim.x * C::KT) * D + p.in_off);
+    }
 #pragma unroll 1
     for (int ct = 0; ct < C::NCT; ++ct) {
       const uint32_t cbase = (w * C::NCT + (uint32_t)ct) * 128u;  // the C tile's first output in the tile
@@ -396,10 +430,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
   __shared__ uint32_t wbad[C::WG / 64];
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
   const float* __restrict__ taps = reinterpret_cast<const float*>(p.taps);
-  const Iq8* __restrict__ in = reinterpret_cast<const Iq8*>(p.in);
   float* __restrict__ out = reinterpret_cast<float*>(p.out);
   const uint32_t T = p.T;
   const int64_t phase = (int64_t)p.out_phase;
+  i8_copy_history(p);
 
   // modulated taps t'_i = t_i e^{j 2 pi (i inc) / 2^32}
   const float t = tid < T ? taps[tid] : 0.0f;
@@ -422,9 +456,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
       for (uint32_t r = tid; r < (uint32_t)C::STRIDE; r += C::WG) {
         const int64_t k = (int64_t)tile * C::STRIDE - phase + r;
         if (k < 0 || (uint64_t)k >= p.N) continue;
-        const float2 y0 = fir_point<float, Iq8, MODE>(p, (uint64_t)k);
+        const float2 y0 = i8_point<MODE>(p, (uint64_t)k);
         if constexpr (MODE == kModeFm) {
-          out[k] = fm_disc(y0, fir_point<float, Iq8, MODE>(p, (uint64_t)k + 1), p.fm_gain);
+          out[k] = fm_disc(y0, i8_point<MODE>(p, (uint64_t)k + 1), p.fm_gain);
         } else {
           out[k] = am_env(y0);
         }
@@ -470,13 +504,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
   const char* bplane = lds + (c ? C::PLANE : 0u);
   const uint32_t w = tid >> 6;
   I8Stage<4, C::SPAN, C::WG> st;
-  if (blockIdx.x < tiles) i8_load_granules<4, VEC>(st, in, ((int64_t)blockIdx.x * C::STRIDE - phase) * D, p.L);
+  if (blockIdx.x < tiles) i8_load_granules<4, VEC>(st, p, ((int64_t)blockIdx.x * C::STRIDE - phase) * D + p.in_off);
   for (uint32_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
     const int64_t k_t = (int64_t)tile * C::STRIDE - phase;  // a multiple of 16 in absolute output index
     i8_store_planes(st, lds, C::PLANE);
     __syncthreads();
     // the next tile's loads fly while this one is computed
-    if (tile + gridDim.x < tiles) i8_load_granules<4, VEC>(st, in, (k_t + (int64_t)gridDim.x * C::STRIDE) * D, p.L);
+    if (tile + gridDim.x < tiles) {
+      i8_load_granules<4, VEC>(st, p, (k_t + (int64_t)gridDim.x * C::STRIDE) * D + p.in_off);
+    }
 #pragma unroll
     for (int ct = 0; ct < C::NCT; ++ct) {
       const uint32_t cbase = (w * C::NCT + (uint32_t)ct) * 64u;

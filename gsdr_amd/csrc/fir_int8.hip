@@ -31,4 +31,37 @@ hipError_t fir_int8_at(uint64_t outputIndex, size_t decimation, const float* tap
   return fir_entry<float, Iq8>(decimation, taps, tapCount, reinterpret_cast<const Iq8*>(input), output, numOutputs,
                                device, stream, -1, (uint32_t)(outputIndex & 15u));
 }
+
+// The streaming object's one-launch step at decimation 4 (stream.hip): outputs [outputIndex, + N) of the
+// stream, output 0's window at chunk offset inOff (negative: it starts in the history buffer), the next
+// history copied by the same launch. Returns hipErrorNotSupported (nothing launched) for shapes that do
+// not take the matrix-core kernel; the stream then takes its seam path.
+hipError_t fir_int8_stream_step(uint64_t outputIndex, const float* taps, size_t tapCount, const int8_t* chunk,
+                                uint64_t chunkLen, int64_t inOff, const int8_t* hist, uint64_t histLen, int8_t* histOut,
+                                int64_t histFrom, uint64_t histN, hipFloatComplex* output, size_t numOutputs,
+                                int32_t device, hipStream_t stream) {
+  if (numOutputs == 0 || tapCount == 0 || taps == nullptr || tapCount > (size_t)I8Mfma<4, 8>::MAXT ||
+      (reinterpret_cast<uintptr_t>(output) % 8) != 0) {
+    return hipErrorNotSupported;
+  }
+  FirJob job;
+  job.in = chunk;
+  job.taps = taps;
+  job.out = output;
+  job.D = 4;
+  job.T = tapCount;
+  job.N = numOutputs;
+  job.L = chunkLen;
+  job.mode = kModeFir;
+  job.out_phase = (uint32_t)(outputIndex & 15u);
+  job.in_off = inOff;
+  job.hist = hist;
+  job.hist_len = histLen;
+  job.hist_out = histOut;
+  job.hist_from = histFrom;
+  job.hist_n = histN;
+  DeviceScope scope(device);
+  if (scope.status() != hipSuccess) return scope.status();
+  return launch_i8_mfma<4, 3>(job, stream);
+}
 }  // namespace gsdr

@@ -126,6 +126,40 @@ static hipError_t chain_multi_entry(int mode, float fs, float tune, const float*
   return hipSuccess;
 }
 
+// The streaming object's one-launch int8 chain step at decimation 4 (stream.hip; see fir_int8_stream_step):
+// firstSampleIndex is the absolute index of output 0's first sample. hipErrorNotSupported: not this path.
+hipError_t chain_int8_stream_step(int mode, float fs, float tune, float chan, float dev, size_t firstSampleIndex,
+                                  const float* taps, size_t tapCount, const int8_t* chunk, uint64_t chunkLen,
+                                  int64_t inOff, const int8_t* hist, uint64_t histLen, int8_t* histOut,
+                                  int64_t histFrom, uint64_t histN, float* output, size_t numOutputs, int32_t device,
+                                  hipStream_t stream) {
+  if (numOutputs == 0 || tapCount == 0 || taps == nullptr || tapCount > (size_t)I8ChainMfma<kModeFm>::MAXT) {
+    return hipErrorNotSupported;
+  }
+  FirJob job;
+  if (!nco_increment(fs, tune, chan, &job.nco_inc)) return hipErrorInvalidValue;
+  job.in = chunk;
+  job.taps = taps;
+  job.out = output;
+  job.D = 4;
+  job.T = tapCount;
+  job.N = numOutputs;
+  job.L = chunkLen;
+  job.mode = mode;
+  job.nco_n0 = (uint32_t)firstSampleIndex;
+  job.out_phase = (uint32_t)((firstSampleIndex / 4) & 15u);
+  if (mode == kModeFm) job.fm_gain = fs / (2.0f * kPiF * dev);
+  job.in_off = inOff;
+  job.hist = hist;
+  job.hist_len = histLen;
+  job.hist_out = histOut;
+  job.hist_from = histFrom;
+  job.hist_n = histN;
+  DeviceScope scope(device);
+  if (scope.status() != hipSuccess) return scope.status();
+  return mode == kModeFm ? launch_chain_i8_mfma<kModeFm>(job, stream) : launch_chain_i8_mfma<kModeAm>(job, stream);
+}
+
 }  // namespace gsdr
 
 GSDR_C_LINKAGE hipError_t gsdrFmDemod(float rfSampleRate, float tuningFrequency, float channelFrequency,

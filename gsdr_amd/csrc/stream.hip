@@ -44,6 +44,16 @@ namespace gsdr {
 hipError_t fir_int8_at(uint64_t outputIndex, size_t decimation, const float* taps, size_t tapCount,
                        const int8_t* input, hipFloatComplex* output, size_t numOutputs, int32_t device,
                        hipStream_t stream);
+hipError_t fir_int8_stream_step(uint64_t outputIndex, const float* taps, size_t tapCount, const int8_t* chunk,
+                                uint64_t chunkLen, int64_t inOff, const int8_t* hist, uint64_t histLen, int8_t* histOut,
+                                int64_t histFrom, uint64_t histN, hipFloatComplex* output, size_t numOutputs,
+                                int32_t device, hipStream_t stream);
+// fm_am.hip (mode 1 = FM, 2 = AM as in fir_engine.hpp)
+hipError_t chain_int8_stream_step(int mode, float fs, float tune, float chan, float dev, size_t firstSampleIndex,
+                                  const float* taps, size_t tapCount, const int8_t* chunk, uint64_t chunkLen,
+                                  int64_t inOff, const int8_t* hist, uint64_t histLen, int8_t* histOut,
+                                  int64_t histFrom, uint64_t histN, float* output, size_t numOutputs, int32_t device,
+                                  hipStream_t stream);
 
 namespace {
 
@@ -178,6 +188,33 @@ GSDR_C_LINKAGE hipError_t gsdrxStreamProcess(gsdrxStream s, const void* input, s
   const uint64_t S = s->consumed, h0 = s->next_out * s->D;
   const uint64_t h = S > h0 ? S - h0 : 0;
   hipError_t e = hipSuccess;
+  if (s->format == GSDRX_SAMPLES_CS8 && s->D == 4 && n_out > 0) {
+    // int8 I/Q at decimation 4: ONE launch of the matrix-core kernel does the seam outputs (their samples
+    // before the chunk read from the history buffer), the direct outputs and the next history copy
+    const int64_t in_off = (int64_t)(s->next_out * s->D) - (int64_t)S;
+    const int64_t from = (int64_t)(p.m_end * s->D) - (int64_t)S;
+    const int8_t* c8 = reinterpret_cast<const int8_t*>(chunk);
+    const int8_t* h8 = reinterpret_cast<const int8_t*>(s->hist);
+    int8_t* n8 = reinterpret_cast<int8_t*>(s->spare);
+    if (s->kind == GSDRX_STREAM_FIR) {
+      e = gsdr::fir_int8_stream_step(s->next_out, s->taps, s->T, c8, numInputSamples, in_off, h8, h, n8, from,
+                                     p.hist_after, reinterpret_cast<hipFloatComplex*>(out), n_out, s->device,
+                                     cudaStream);
+    } else {
+      e = gsdr::chain_int8_stream_step(s->kind == GSDRX_STREAM_FM ? 1 : 2, s->fs, s->tune, s->chan, s->dev,
+                                       s->n0 + h0, s->taps, s->T, c8, numInputSamples, in_off, h8, h, n8, from,
+                                       p.hist_after, reinterpret_cast<float*>(out), n_out, s->device, cudaStream);
+    }
+    if (e == hipSuccess) {
+      std::swap(s->hist, s->spare);
+      s->consumed += numInputSamples;
+      s->next_out = p.m_end;
+      if (numOutputsWritten) *numOutputsWritten = n_out;
+      return hipSuccess;
+    }
+    if (e != hipErrorNotSupported) return e;
+    e = hipSuccess;  // not this shape: the seam path below
+  }
   if (p.n_seam) {
     e = gsdr::copy(s->seam, s->hist, h * s->sb, cudaStream);
     if (e == hipSuccess) e = gsdr::copy(s->seam + h * s->sb, chunk, p.head * s->sb, cudaStream);

@@ -515,3 +515,45 @@ def test_int8_mfma_shift_invariant(cuda, kind):
             src = buf
         got = host(fn(src, td, *args, D, n0 + D * k0, n, out=out))
         assert got.tobytes() == whole[k0:k0 + n].tobytes(), k0
+
+
+@pytest.mark.parametrize("kind", ["fir", "fm", "am"])
+@pytest.mark.parametrize("case", ["inf_tap", "nan_tap", "impulses"])
+def test_int8_stream_one_launch(cuda, kind, case):
+    """int8 streams at decimation 4 run one matrix-core launch a call: the seam outputs read their samples
+    before the chunk from the history buffer and the same launch writes the next history. Chunked ==
+    monolithic bit for bit, for taps that are not finite (the exact per-output fallback, which reads the
+    history as well) and for an impulse train, over chunk sizes from 1 sample up."""
+    from gsdr_amd import ops
+    from gsdr_amd.signals import fm_test_signal, lowpass_taps
+    from gsdr_amd.stream import Stream
+
+    D, T, n0 = 4, 127, 77_777_777
+    fs, tune, chan, dhz = 1.0e6, 0.0, 1.0e5, 2.0e4
+    L = 40_000 + 3
+    taps = lowpass_taps(T, 0.1).copy()
+    if case == "impulses":
+        x8 = impulse_train(L, 131, seed=11)
+    else:
+        x = fm_test_signal(L, noise=0.02, n0=n0)
+        x8 = np.clip(np.round(np.stack([x.real, x.imag], 1).ravel() * 100), -128, 127).astype(np.int8)
+        taps[40] = np.inf if case == "inf_tap" else np.nan
+    xd, td = dev(x8, cuda), dev(taps, cuda)
+    if kind == "fir":
+        want = ops.fir(td, xd, D)
+    elif kind == "fm":
+        want = ops.fm_demod(xd, td, fs, tune, chan, dhz, D, n0)
+    else:
+        want = ops.am_demod(xd, td, fs, tune, chan, D, n0)
+    s = Stream(kind, td, D, fs, tune, chan, dhz, first_sample_index=n0, int8=True)
+    parts, pos = [], 0
+    rng = np.random.default_rng(len(kind) + len(case))
+    while pos < L:
+        m = min(L - pos, int(rng.choice([1, 2, 3, 5, T - 1, T + 7, 333, 4096, 17001])))
+        parts.append(s.process(xd[2 * pos:2 * (pos + m)]).clone())
+        pos += m
+    s.close()
+    got = torch.cat(parts)
+    torch.cuda.synchronize()
+    assert got.numel() == want.numel()
+    assert got.cpu().numpy().tobytes() == want.cpu().numpy().tobytes()

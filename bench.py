@@ -548,49 +548,54 @@ def secondary_configs(torch, ops, device, taps):
     return out, c5
 
 
-def int8_stream_rate(torch, abi, device, taps, x8s, stream, t_call, chunks=8):
+def int8_stream_rate(torch, abi, device, taps, x8s, stream, t_call, chunk_counts=(1, 2, 8)):
     """SURVEY.md 8(f) rows 1 + 2: config 2's int8 channel fed through a gsdrxStream (CS8 FIR, D = 4) in
-    `chunks` equal chunks per pass (seam launches, direct launches and history copies included), passes
-    rotating over the batches, against one gsdrxFirFCInt8 call (t_call) -- the streaming object runs the
-    same matrix-core kernel, its blocks aligned to the stream's output index."""
+    C equal chunks per pass, passes rotating over the batches, against one gsdrxFirFCInt8 call (t_call).
+    At decimation 4 every gsdrxStreamProcess call is ONE launch of the same matrix-core kernel (seam
+    samples from the history buffer, next history written by the launch), so the difference is the
+    per-launch fixed cost (~6.5 us: launch, tap split, first tile's load latency) times C, and the host's
+    issue time per call (host_us_per_call, measured over the same loop)."""
     import ctypes
 
-    h = ctypes.c_void_p()
-    rc = abi.lib.gsdrxStreamCreate(ctypes.byref(h), 0, 1, DECIM, taps.data_ptr(), TAPS, 1.0, 0.0, 0.0, 1.0, 0,
-                                   device.index)
-    assert rc == 0, rc
-    cs = N_IN // chunks
-    y = torch.empty(N_OUT + 16, dtype=torch.complex64, device=device)
+    res = {"config": "config 2's int8 I/Q channel through gsdrxStream (CS8 FIR, D = 4), C chunks a pass",
+           "single_call_us": round(t_call * 1e6, 2)}
+    y = torch.empty(N_OUT + 1024, dtype=torch.complex64, device=device)  # a call can emit the history's outputs too
+    yp, ycap = y.data_ptr(), y.numel()
     written = ctypes.c_size_t()
-    argsets = []
-    for x in x8s:
-        for c in range(chunks):
-            n = cs if c < chunks - 1 else N_IN - cs * (chunks - 1)
-            argsets.append([x.data_ptr() + 2 * cs * c, n])
-    cnt = [0]
-
-    def one_pass():
-        for _ in range(chunks):
-            p, n = argsets[cnt[0] % len(argsets)]
-            cnt[0] += 1
-            r = abi.lib.gsdrxStreamProcess(h, p, n, y.data_ptr(), y.numel(), ctypes.byref(written), stream)
-            assert r == 0, r
-
-    for _ in range(20):
-        one_pass()
-    torch.cuda.synchronize()
-    reps = 50
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        one_pass()
-    e1.record()
-    torch.cuda.synchronize()
-    t = e0.elapsed_time(e1) / reps * 1e-3
-    abi.lib.gsdrxStreamDestroy(h)
-    return {"config": f"config 2's int8 I/Q channel through gsdrxStream (CS8 FIR, D = 4) in {chunks} chunks a pass",
-            "us_per_channel": round(t * 1e6, 2), "msamples_per_s": round(N_IN / t / 1e6, 1),
-            "vs_single_call": round(t_call / t, 3)}
+    wref = ctypes.byref(written)
+    for chunks in chunk_counts:
+        h = ctypes.c_void_p()
+        rc = abi.lib.gsdrxStreamCreate(ctypes.byref(h), 0, 1, DECIM, taps.data_ptr(), TAPS, 1.0, 0.0, 0.0, 1.0, 0,
+                                       device.index)
+        assert rc == 0, rc
+        cs = N_IN // chunks
+        argsets = []
+        for x in x8s:
+            for c in range(chunks):
+                n = cs if c < chunks - 1 else N_IN - cs * (chunks - 1)
+                argsets.append((h, x.data_ptr() + 2 * cs * c, n, yp, ycap, wref, stream))
+        fn = abi.lib.gsdrxStreamProcess
+        k = 0
+        for _ in range(max(20, 8 * chunks)):
+            assert fn(*argsets[k % len(argsets)]) == 0
+            k += 1
+        torch.cuda.synchronize()
+        calls = 50 * chunks
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        h0 = time.perf_counter()
+        for _ in range(calls):
+            fn(*argsets[k % len(argsets)])
+            k += 1
+        h1 = time.perf_counter()
+        e1.record()
+        torch.cuda.synchronize()
+        t = e0.elapsed_time(e1) / calls * chunks * 1e-3  # per channel pass
+        abi.lib.gsdrxStreamDestroy(h)
+        res[f"{chunks}_chunks"] = {"us_per_channel": round(t * 1e6, 2), "msamples_per_s": round(N_IN / t / 1e6, 1),
+                                   "vs_single_call": round(t_call / t, 3),
+                                   "host_us_per_call": round((h1 - h0) / calls * 1e6, 2)}
+    return res
 
 
 def sq_rule_disagreements(torch, rx, ctype, chunk=1 << 19):

@@ -297,23 +297,24 @@ hipError_t launch_i8_mfma_ns(const FirJob& j, hipStream_t s) {
   const uint32_t ns = (uint32_t)ceil_div<uint64_t>(15u * D + j.T, 32u);
   const uint64_t tiles = ceil_div<uint64_t>(j.N + p.out_phase, (uint64_t)C::KT);
   if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
-  int dev = 0, cus = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  int cus = 0;
+  const hipError_t e = current_device_cus(&cus);
   if (e != hipSuccess) return e;
   const uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)cus * BPC);
   // tile starts are at sample (j KT - phase) D + in_off: byte offset 2 D (j KT - phase) + 2 in_off
   const uintptr_t in0 = reinterpret_cast<uintptr_t>(j.in) + (uintptr_t)(2 * j.in_off) - 2u * D * p.out_phase;
   const bool oa = ((reinterpret_cast<uintptr_t>(j.out) - 8u * p.out_phase) % 16) == 0;
-#define GSDR_I8_LAUNCH(G, VEC)                                                                             \
-  (oa ? (k_fir_i8_mfma<D, NS, G, VEC, true, BPC><<<dim3(grid), dim3(C::WG), 0, s>>>(p, ns, (uint32_t)tiles), 0) \
-      : (k_fir_i8_mfma<D, NS, G, VEC, false, BPC><<<dim3(grid), dim3(C::WG), 0, s>>>(p, ns, (uint32_t)tiles), 0))
+#define GSDR_I8_LAUNCH(G, LM)                                                                              \
+  (oa ? (k_fir_i8_mfma<D, NS, G, LM, true, BPC><<<dim3(grid), dim3(C::WG), 0, s>>>(p, ns, (uint32_t)tiles), 0) \
+      : (k_fir_i8_mfma<D, NS, G, LM, false, BPC><<<dim3(grid), dim3(C::WG), 0, s>>>(p, ns, (uint32_t)tiles), 0))
   if (in0 % 16 == 0) {
-    (void)GSDR_I8_LAUNCH(8, true);
+    (void)GSDR_I8_LAUNCH(8, 1);
   } else if (in0 % 8 == 0) {
-    (void)GSDR_I8_LAUNCH(4, true);
+    (void)GSDR_I8_LAUNCH(4, 1);
+  } else if (in0 % 2 == 0) {
+    (void)GSDR_I8_LAUNCH(4, 2);  // 2-byte aligned: shifted 8-byte loads
   } else {
-    (void)GSDR_I8_LAUNCH(8, false);
+    (void)GSDR_I8_LAUNCH(8, 0);
   }
 #undef GSDR_I8_LAUNCH
   return launch_status();
@@ -345,16 +346,18 @@ hipError_t launch_chain_i8_mfma(const FirJob& j, hipStream_t s) {
   const uint32_t ns = (uint32_t)ceil_div<uint64_t>(7u * 4u + j.T, 32u);
   const uint64_t tiles = ceil_div<uint64_t>(j.N + p.out_phase, (uint64_t)C::STRIDE);
   if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
-  int dev = 0, cus = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  int cus = 0;
+  const hipError_t e = current_device_cus(&cus);
   if (e != hipSuccess) return e;
   const uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)cus * BPC);
   // tile starts are at sample 4 (j STRIDE - phase) + in_off: 8 (j STRIDE - phase) + 2 in_off bytes
-  if (((reinterpret_cast<uintptr_t>(j.in) + (uintptr_t)(2 * j.in_off)) % 8) == 0) {
-    k_chain_i8_mfma<MODE, true, BPC, NCT><<<dim3(grid), dim3(C::WG), 0, s>>>(p, ns, (uint32_t)tiles);
+  const uintptr_t in0 = reinterpret_cast<uintptr_t>(j.in) + (uintptr_t)(2 * j.in_off);
+  if (in0 % 8 == 0) {
+    k_chain_i8_mfma<MODE, 1, BPC, NCT><<<dim3(grid), dim3(C::WG), 0, s>>>(p, ns, (uint32_t)tiles);
+  } else if (in0 % 2 == 0) {  // 2-byte aligned: shifted 8-byte loads
+    k_chain_i8_mfma<MODE, 2, BPC, NCT><<<dim3(grid), dim3(C::WG), 0, s>>>(p, ns, (uint32_t)tiles);
   } else {
-    k_chain_i8_mfma<MODE, false, BPC, NCT><<<dim3(grid), dim3(C::WG), 0, s>>>(p, ns, (uint32_t)tiles);
+    k_chain_i8_mfma<MODE, 0, BPC, NCT><<<dim3(grid), dim3(C::WG), 0, s>>>(p, ns, (uint32_t)tiles);
   }
   return launch_status();
 }

@@ -166,15 +166,19 @@ struct I8Stage {
   uint32_t wv[NGR][NW];
 };
 
-template <int G, bool VEC, int SPAN, int WG>
+// LM (load mode): 1 = the tile starts are G * 2-byte aligned (one vector load a granule); 2 = they are
+// 2-byte aligned only (G = 4: a chunk of a stream that ended on an odd sample count): two aligned 8-byte
+// loads a granule and a funnel shift (v_alignbit_b32) by the sample offset; 0 = per-sample loads.
+// Interior tiles (all but the first and last of a launch) need no per-granule bounds: a uniform base plus a
+// 32-bit lane offset per load.
+template <int G, int LM, int SPAN, int WG>
 __device__ __forceinline__ void i8_load_granules(I8Stage<G, SPAN, WG>& st, const FirParams& p, int64_t S0) {
+  static_assert(LM != 2 || G == 4, "shifted loads move 4-sample granules");
   const Iq8* __restrict__ in = reinterpret_cast<const Iq8*>(p.in);
   const uint64_t L = p.L;
   using S = I8Stage<G, SPAN, WG>;
   const uint32_t tid = threadIdx.x;
-  if (VEC && S0 >= 0 && (uint64_t)S0 + SPAN <= L) {
-    // interior tile (all but the first and last): no per-granule bounds, a uniform base plus a 32-bit lane
-    // offset per load
+  if (LM == 1 && S0 >= 0 && (uint64_t)S0 + SPAN <= L) {
     const char* base = reinterpret_cast<const char*>(in + S0);
 #pragma unroll
     for (uint32_t r = 0; r < S::NGR; ++r) {
@@ -193,6 +197,29 @@ __device__ __forceinline__ void i8_load_granules(I8Stage<G, SPAN, WG>& st, const
     }
     return;
   }
+  if constexpr (LM == 2) {
+    const uint32_t dl = (uint32_t)((reinterpret_cast<uintptr_t>(in + S0) >> 1) & 3u);  // samples past 8-byte alignment
+    if (S0 >= (int64_t)dl && (uint64_t)S0 + SPAN + 4 <= L) {
+      const char* base = reinterpret_cast<const char*>(in + S0) - 2 * dl;  // 8-byte aligned
+      const bool up = dl >= 2;                   // the wanted dwords start in the second dword
+      const uint32_t sh = (dl & 1u) ? 16u : 0u;  // and half a dword further
+#pragma unroll
+      for (uint32_t r = 0; r < S::NGR; ++r) {
+        const uint32_t g = tid + r * WG;
+        if (r + 1 < S::NGR || g < S::NG) {
+          const gsdr_u2v a = __builtin_nontemporal_load(reinterpret_cast<const gsdr_u2v*>(base + 8u * g));
+          const gsdr_u2v b = __builtin_nontemporal_load(reinterpret_cast<const gsdr_u2v*>(base + 8u * g + 8u));
+          const uint32_t d0 = up ? a.y : a.x, d1 = up ? b.x : a.y, d2 = up ? b.y : b.x;
+          st.wv[r][0] = __builtin_amdgcn_alignbit(d1, d0, sh);
+          st.wv[r][1] = __builtin_amdgcn_alignbit(d2, d1, sh);
+        }
+      }
+      return;
+    }
+  }
+  // edge tiles: granule by granule, vector loads where the granule (and, shifted, its aligned cover) lies in
+  // the input
+  const uint32_t dl2 = LM == 2 ? (uint32_t)((reinterpret_cast<uintptr_t>(in + S0) >> 1) & 3u) : 0u;
 #pragma unroll
   for (uint32_t r = 0; r < S::NGR; ++r) {
     const uint32_t g = tid + r * WG;
@@ -200,7 +227,7 @@ __device__ __forceinline__ void i8_load_granules(I8Stage<G, SPAN, WG>& st, const
 #pragma unroll
     for (int k = 0; k < S::NW; ++k) st.wv[r][k] = 0u;
     if (g < S::NG) {
-      if (VEC && s >= 0 && (uint64_t)s + G <= L) {
+      if (LM == 1 && s >= 0 && (uint64_t)s + G <= L) {
         if constexpr (G == 8) {
           const gsdr_u4v t = __builtin_nontemporal_load(reinterpret_cast<const gsdr_u4v*>(in + s));
 #pragma unroll
@@ -210,6 +237,15 @@ __device__ __forceinline__ void i8_load_granules(I8Stage<G, SPAN, WG>& st, const
           st.wv[r][0] = t.x;
           st.wv[r][1] = t.y;
         }
+      } else if (LM == 2 && s >= (int64_t)dl2 && (uint64_t)s - dl2 + 8 <= L) {
+        const char* a8 = reinterpret_cast<const char*>(in + s) - 2 * dl2;
+        const gsdr_u2v a = __builtin_nontemporal_load(reinterpret_cast<const gsdr_u2v*>(a8));
+        const gsdr_u2v b = __builtin_nontemporal_load(reinterpret_cast<const gsdr_u2v*>(a8 + 8));
+        const bool up = dl2 >= 2;
+        const uint32_t sh = (dl2 & 1u) ? 16u : 0u;
+        const uint32_t d0 = up ? a.y : a.x, d1 = up ? b.x : a.y, d2 = up ? b.y : b.x;
+        st.wv[r][0] = __builtin_amdgcn_alignbit(d1, d0, sh);
+        st.wv[r][1] = __builtin_amdgcn_alignbit(d2, d1, sh);
       } else {  // input ends, unaligned input or samples before the buffer: per-sample loads
 #pragma unroll
         for (int k = 0; k < S::NW; ++k) {
@@ -276,8 +312,8 @@ struct I8Mfma {
 };
 
 // BPC workgroups per CU (one wave per SIMD each): the register budget is 512 / BPC VGPRs.
-// G / VEC: staging granule (I8Stage); OA: the output pairs (k, k + 1) are 16-byte aligned.
-template <int D, int NS, int G, bool VEC, bool OA, int BPC>
+// G / LM: staging granule and load mode (I8Stage, i8_load_granules); OA: the output pairs (k, k + 1) are 16-byte aligned.
+template <int D, int NS, int G, int LM, bool OA, int BPC>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC))) void k_fir_i8_mfma(FirParams p, uint32_t ns, uint32_t tiles) {
   using C = I8Mfma<D, NS>;
   __shared__ __attribute__((aligned(16))) char lds[C::LDS_BYTES];
@@ -339,14 +375,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
   const int n = (int)(lane & 15u), q = (int)(lane >> 4), c = n & 1, b = n >> 1;
   const char* bplane = lds + (c ? C::PLANE : 0u);
   I8Stage<G, C::SPAN, C::WG> st;
-  if (blockIdx.x < tiles) i8_load_granules<G, VEC>(st, p, ((int64_t)blockIdx.x * C::KT - phase) * D + p.in_off);
+  if (blockIdx.x < tiles) i8_load_granules<G, LM>(st, p, ((int64_t)blockIdx.x * C::KT - phase) * D + p.in_off);
   for (uint32_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
     const int64_t k_t = (int64_t)tile * C::KT - phase;  // a multiple of 16 in absolute output index
     i8_store_planes(st, lds, C::PLANE);
     __syncthreads();
     // the next tile's loads fly while this one is computed
     if (tile + gridDim.x < tiles) {
-      i8_load_granules<G, VEC>(st, p, (k_t + (int64_t)gridDim.x * C::KT) * D + p.in_off);
+      i8_load_granules<G, LM>(st, p, (k_t + (int64_t)gridDim.x * C::KT) * D + p.in_off);
     }
 #pragma unroll 1
     for (int ct = 0; ct < C::NCT; ++ct) {
@@ -420,7 +456,7 @@ struct I8ChainMfma {
   static constexpr uint32_t LDS_BYTES = PLANE + addr(SPAN);
 };
 
-template <int MODE, bool VEC, int BPC, int NCT>
+template <int MODE, int LM, int BPC, int NCT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC))) void k_chain_i8_mfma(FirParams p, uint32_t ns, uint32_t tiles) {
   using C = I8ChainMfma<MODE, NCT>;
   constexpr int D = C::D;
@@ -504,14 +540,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
   const char* bplane = lds + (c ? C::PLANE : 0u);
   const uint32_t w = tid >> 6;
   I8Stage<4, C::SPAN, C::WG> st;
-  if (blockIdx.x < tiles) i8_load_granules<4, VEC>(st, p, ((int64_t)blockIdx.x * C::STRIDE - phase) * D + p.in_off);
+  if (blockIdx.x < tiles) i8_load_granules<4, LM>(st, p, ((int64_t)blockIdx.x * C::STRIDE - phase) * D + p.in_off);
   for (uint32_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
     const int64_t k_t = (int64_t)tile * C::STRIDE - phase;  // a multiple of 16 in absolute output index
     i8_store_planes(st, lds, C::PLANE);
     __syncthreads();
     // the next tile's loads fly while this one is computed
     if (tile + gridDim.x < tiles) {
-      i8_load_granules<4, VEC>(st, p, (k_t + (int64_t)gridDim.x * C::STRIDE) * D + p.in_off);
+      i8_load_granules<4, LM>(st, p, (k_t + (int64_t)gridDim.x * C::STRIDE) * D + p.in_off);
     }
 #pragma unroll
     for (int ct = 0; ct < C::NCT; ++ct) {

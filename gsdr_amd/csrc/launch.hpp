@@ -7,6 +7,8 @@
 // even when a launch failed, cuh:90-93).
 #pragma once
 
+#include <atomic>
+
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
@@ -41,6 +43,25 @@ class DeviceScope {
   bool switched_ = false;
   hipError_t status_ = hipSuccess;
 };
+
+// Compute units of the current device, cached per device index (the persistent kernels size their grid
+// by it on every launch; the attribute query is a host round trip worth avoiding on small calls).
+inline hipError_t current_device_cus(int* cus) noexcept {
+  static std::atomic<int> cache[64] = {};
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev >= 0 && dev < 64) {
+    const int c = cache[dev].load(std::memory_order_relaxed);
+    if (c > 0) {
+      *cus = c;
+      return hipSuccess;
+    }
+  }
+  e = hipDeviceGetAttribute(cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e == hipSuccess && dev >= 0 && dev < 64) cache[dev].store(*cus, std::memory_order_relaxed);
+  return e;
+}
 
 // Status of the most recent launch on this thread. hipGetLastError also clears the sticky
 // per-thread error so a later call does not report a stale failure.

@@ -10,7 +10,7 @@ HIPFLAGS := -O3 -std=c++17 -fPIC -ffp-contract=off --offload-arch=$(ARCH) -fvisi
 OFLAGS  := -O2 -std=c11 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wextra -Ioracle -mfma
 
 SRCS := $(wildcard gsdr_amd/csrc/*.hip)
-HDRS := $(wildcard gsdr_amd/csrc/*.hpp) $(wildcard include/gsdr/*.h)
+HDRS := $(wildcard gsdr_amd/csrc/*.hpp) $(wildcard gsdr_amd/csrc/*.inc) $(wildcard include/gsdr/*.h)
 OBJS := $(patsubst gsdr_amd/csrc/%.hip,$(BUILD)/%.o,$(SRCS))
 
 all: gsdr_amd/libgsdr.so oracle/build/liboracle.so examples probes
@@ -33,7 +33,7 @@ $(BUILD)/probes/fir.o: gsdr_amd/csrc/fir.hip $(HDRS)
 $(BUILD)/probes/libgsdr_probes.so: $(filter-out $(BUILD)/fir.o,$(OBJS)) $(BUILD)/probes/fir.o
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -Wl,-rpath,/opt/rocm/lib $^ -o $@
 
-oracle/build/liboracle.so: oracle/gsdr_oracle.c oracle/gsdr_oracle.h
+oracle/build/liboracle.so: oracle/gsdr_oracle.c oracle/gsdr_oracle.h gsdr_amd/csrc/awgn_table.inc
 	@mkdir -p oracle/build
 	$(CC) $(OFLAGS) -shared oracle/gsdr_oracle.c -o $@ -lm -lpthread
 

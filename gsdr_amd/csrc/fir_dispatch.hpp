@@ -420,10 +420,17 @@ hipError_t launch_rt_wg(const FirJob& j, uint32_t nch, size_t lds, hipStream_t s
   if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
   constexpr uint64_t A = SampleT<InT>::kSrcAlign;
   const bool vec = (reinterpret_cast<uintptr_t>(j.in) % A) == 0 && ((uint64_t)stride * j.D * sizeof(InT)) % A == 0;
-  if (vec) {
-    k_fir_rt<TapT, InT, IC, WG, true, MODE><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
+  const dim3 grid((uint32_t)tiles), block(WG);
+  if (j.D % 2 == 0) {  // paired LDS reads (k_fir_rt): same products, same order
+    if (vec) {
+      k_fir_rt<TapT, InT, IC, WG, true, MODE, true><<<grid, block, lds, s>>>(p);
+    } else {
+      k_fir_rt<TapT, InT, IC, WG, false, MODE, true><<<grid, block, lds, s>>>(p);
+    }
+  } else if (vec) {
+    k_fir_rt<TapT, InT, IC, WG, true, MODE><<<grid, block, lds, s>>>(p);
   } else {
-    k_fir_rt<TapT, InT, IC, WG, false, MODE><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
+    k_fir_rt<TapT, InT, IC, WG, false, MODE><<<grid, block, lds, s>>>(p);
   }
   return launch_status();
 }

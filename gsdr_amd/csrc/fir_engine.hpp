@@ -1061,13 +1061,36 @@ __global__ __launch_bounds__(WG) void k_fir_contig(FirParams p) {
 // as an immediate offset), in ascending tap order like the generic kernel. No register window (D is
 // not known at compile time), so it is bound by LDS reads (~T * sample bytes per output), which
 // still beats re-reading every sample T / D times through L1/L2.
+// PAIR (even D): two consecutive samples per LDS read (complex: ds_read_b128, real: ds_read_b64), still
+// multiplied in ascending tap order. One sample a read puts lane t at bank 2Dt mod 64 (complex), which
+// for D = 2^k m (m odd) touches only 64 / 2^k of the banks: 2-way conflicts at D = 50, 4-way at 100
+// (PMC: 42 % of LDS cycles at D = 50, profiles/r01_pmc_fir_rt_d50_d13.txt). ds_read_b128 serves 16
+// lanes a cycle with lane groups whose indices cover every residue mod 16, so lane starts 4(D/2)t mod 64
+// are distinct for D = 2 mod 4 (conflict-free) and 2-way at D = 4 mod 8; half the read instructions too.
 // ------------------------------------------------------------------------------------------------
-template <class TapT, class InT, int IC, int WG, bool VEC, int MODE>
+template <class LdsT>
+struct LdsPair;
+template <>
+struct LdsPair<float> {
+  using type = float2;
+  __device__ static float lo(float2 v) { return v.x; }
+  __device__ static float hi(float2 v) { return v.y; }
+};
+template <>
+struct LdsPair<float2> {
+  using type = float4;
+  __device__ static float2 lo(float4 v) { return make_float2(v.x, v.y); }
+  __device__ static float2 hi(float4 v) { return make_float2(v.z, v.w); }
+};
+
+template <class TapT, class InT, int IC, int WG, bool VEC, int MODE, bool PAIR = false>
 __global__ __launch_bounds__(WG) void k_fir_rt(FirParams p) {
   using OutT = typename Product<TapT, InT>::type;
   using LdsT = typename LdsSample<InT>::type;
   constexpr int G = SampleT<InT>::kPerGranule;
-  constexpr int SB = 4;  // granules in flight per lane while staging
+  // granules in flight per lane while staging: the tile (D * WG samples) bounds the resident workgroups to
+  // 1-2 waves a SIMD at large D, so each lane keeps 16 loads (256 B) in flight (4: D = 50 FC 125 us)
+  constexpr int SB = 16;
 
   extern __shared__ __attribute__((aligned(16))) float4 lds[];
   const InT* __restrict__ in = reinterpret_cast<const InT*>(p.in);
@@ -1101,8 +1124,20 @@ __global__ __launch_bounds__(WG) void k_fir_rt(FirParams p) {
 #pragma unroll
     for (int i = 0; i < IC; ++i) tv[i] = tap_at<TapT>(tb, i);
     const LdsT* __restrict__ xc = xs + c * IC;
+    if constexpr (PAIR) {
+      static_assert(IC % 2 == 0, "pairs of taps");
+      using P = LdsPair<LdsT>;
+      const typename P::type* __restrict__ xp = reinterpret_cast<const typename P::type*>(xc);  // D even: aligned
 #pragma unroll
-    for (int i = 0; i < IC; ++i) mac(acc, xc[i], tv[i]);
+      for (int i = 0; i < IC / 2; ++i) {
+        const typename P::type v = xp[i];
+        mac(acc, P::lo(v), tv[2 * i]);
+        mac(acc, P::hi(v), tv[2 * i + 1]);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < IC; ++i) mac(acc, xc[i], tv[i]);
+    }
   }
   OutT accs[1] = {acc};
   if (!finite_out(acc)) ascending_fixup<TapT, InT, NoPad, false, 1>(lds, p, D, tid, accs);

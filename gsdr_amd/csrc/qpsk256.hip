@@ -229,38 +229,80 @@ __global__ __launch_bounds__(kCBlock) void k_c256_mod(C256Streams st, uint32_t n
 // Modulate + counter-based AWGN (gsdrxQpsk256ModulateAwgn; awgn.hpp). One Philox block serves three
 // symbols, so a lane takes six consecutive symbols a step: two blocks when the first absolute index is a
 // multiple of 3 (R3 = firstSymbolIndex % 3, uniform, a template parameter so every slot and block index
-// is a compile-time constant), three otherwise. Three 16-byte stores a lane (48-byte lane stride).
+// is a compile-time constant), three otherwise. A wave's 384 noisy symbols (3 KB) go through LDS so that
+// each of its three 16-byte store instructions writes 1 KB contiguous: stored straight from the lanes
+// (48-byte lane stride) they ran at about half the copy rate, which bound the kernel once the normals
+// were cheap (the write-heavy maps of section 3.6 showed the same).
 constexpr int kAwgnSym = 6;    // symbols per lane per step
 constexpr int kAwgnSteps = 3;  // steps per workgroup
+constexpr uint32_t kAwgnWaveSyms = 64u * kAwgnSym;
 constexpr uint32_t kAwgnBlockSyms = kCBlock * kAwgnSym * kAwgnSteps;
+
+// LDS hand-off between the lanes of one wave: without it the compiler, reasoning per thread, may
+// forward a lane's own earlier LDS store to its later load past another lane's store.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 template <int R3>
 __global__ __launch_bounds__(kCBlock) void k_c256_mod_awgn(const uint8_t* __restrict__ in, float2* __restrict__ out,
                                                             uint32_t n, uint32_t type, float sigma, uint64_t seed,
                                                             uint64_t first) {
   __shared__ float2 tab[256];
-  load_table(tab, type);
+  __shared__ float2 ntab[kAwgnTableSize];
+  __shared__ float4 stage[kCBlock / 64][kAwgnWaveSyms / 2];  // per wave: 384 symbols as 192 float4
+  awgn_load_table(ntab, kCBlock);
+  load_table(tab, type);  // its barrier publishes both tables
   constexpr int NB = R3 == 0 ? 2 : 3;  // Philox blocks touched by six symbols starting at slot R3
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  float4* __restrict__ st = stage[wv];
+  // 16-byte aligned output: the wave's stores can be whole float4s (every wave step starts at a multiple
+  // of 384 symbols from `out`)
+  const bool aligned = (reinterpret_cast<uintptr_t>(out) & 15u) == 0;
+  const bool in_even = (reinterpret_cast<uintptr_t>(in) & 1u) == 0;
   const uint64_t base = (uint64_t)blockIdx.x * kAwgnBlockSyms;
 #pragma unroll 1
   for (int it = 0; it < kAwgnSteps; ++it) {
-    const uint64_t s = base + (uint64_t)kAwgnSym * ((uint32_t)it * kCBlock + threadIdx.x);  // local first symbol
-    if (s >= n) break;
-    const uint64_t b0 = (first + s) / 3u;  // (first + s) % 3 == R3: s is a multiple of 6
+    const uint64_t ws = base + (uint64_t)kAwgnWaveSyms * ((uint32_t)it * (kCBlock / 64) + wv);  // wave's first
+    if (ws >= n) break;
+    const uint64_t s = ws + (uint64_t)kAwgnSym * lane;  // this lane's first symbol (a multiple of 6)
+    const bool whole = ws + kAwgnWaveSyms <= n;          // wave-uniform
+    const uint64_t b0 = (first + s) / 3u;  // (first + s) % 3 == R3
     uint32_t w[NB][4];
 #pragma unroll
     for (int b = 0; b < NB; ++b) awgn_block_words(seed, b0 + b, w[b]);
+    uint8_t sym[kAwgnSym];
+    if (whole && in_even) {  // three 2-byte loads (s is even)
+      const uint16_t* __restrict__ in2 = reinterpret_cast<const uint16_t*>(in + s);
+#pragma unroll
+      for (int q = 0; q < kAwgnSym / 2; ++q) {
+        const uint16_t v = in2[q];
+        sym[2 * q] = (uint8_t)v;
+        sym[2 * q + 1] = (uint8_t)(v >> 8);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < kAwgnSym; ++j) sym[j] = s + j < n ? in[s + j] : 0;
+    }
     float2 y[kAwgnSym];
 #pragma unroll
     for (int j = 0; j < kAwgnSym; ++j) {
-      const float2 g = awgn_slot(w[(R3 + j) / 3], (R3 + j) % 3);
-      const float2 p = s + j < n ? tab[in[s + j]] : make_float2(0.0f, 0.0f);
+      const float2 g = awgn_slot(ntab, w[(R3 + j) / 3], (R3 + j) % 3);
+      const float2 p = tab[sym[j]];
       y[j] = make_float2(p.x + sigma * g.x, p.y + sigma * g.y);
     }
-    if (s + kAwgnSym <= n && (reinterpret_cast<uintptr_t>(out + s) & 15u) == 0) {
-      float4* o = reinterpret_cast<float4*>(out + s);
+    if (whole && aligned) {
 #pragma unroll
-      for (int q = 0; q < kAwgnSym / 2; ++q) o[q] = make_float4(y[2 * q].x, y[2 * q].y, y[2 * q + 1].x, y[2 * q + 1].y);
+      for (int q = 0; q < kAwgnSym / 2; ++q) {
+        st[lane * 3 + q] = make_float4(y[2 * q].x, y[2 * q].y, y[2 * q + 1].x, y[2 * q + 1].y);
+      }
+      wave_sync();
+      float4* __restrict__ o = reinterpret_cast<float4*>(out + ws);
+#pragma unroll
+      for (int q = 0; q < kAwgnSym / 2; ++q) o[q * 64 + lane] = st[q * 64 + lane];
+      wave_sync();  // the next step's LDS writes come after every lane's reads
     } else {
 #pragma unroll
       for (int j = 0; j < kAwgnSym; ++j) {
@@ -270,13 +312,6 @@ __global__ __launch_bounds__(kCBlock) void k_c256_mod_awgn(const uint8_t* __rest
   }
 }
 
-// LDS hand-off between the lanes of one wave: without it the compiler, reasoning per thread, may
-// forward a lane's own earlier LDS store to its later load past another lane's store.
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 // TYPE 0: rectangular table (per-axis fast path); TYPE 1: circular table (per-cell candidate lists).
 // Both fall back to the exhaustive search for inputs their fast path does not cover.

@@ -196,9 +196,11 @@ GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxAmDemodMulti(
  * additive white Gaussian noise of standard deviation `sigma` per axis, in one pass:
  *     output[k] = table[inputBytes[k]] + (fl(sigma * g0), fl(sigma * g1)),  per component the product
  *     rounded, then the sum rounded (two roundings, no fused multiply-add),
- * where (g0, g1) are the standard normals of absolute symbol index firstSymbolIndex + k: Box-Muller
- * over Philox4x32-10 keyed by `seed` (the exact construction is in gsdr_amd/csrc/awgn.hpp and its host
- * restatement in oracle/gsdr_oracle.h), built from correctly rounded IEEE operations only. The noise
+ * where (g0, g1) are the standard normals of absolute symbol index firstSymbolIndex + k: 21 bits of
+ * Philox4x32-10 keyed by `seed` per normal, mapped by inverse-CDF interpolation in a 672-entry
+ * half-normal quantile table (within 2.5e-5 of the exact quantile, tails cut at 5.035; the exact
+ * construction is in gsdr_amd/csrc/awgn.hpp and its host restatement in oracle/gsdr_oracle.h), built
+ * from exact integer operations and one correctly rounded fmaf. The noise
  * is therefore a pure function of (seed, absolute index): a host can regenerate the noisy buffer bit
  * for bit, and splitting a buffer over several calls (advancing firstSymbolIndex) yields the same
  * samples. Returns hipErrorInvalidValue for null pointers or a negative / non-finite sigma.

@@ -489,75 +489,29 @@ static uint32_t f_bits(float f) {
   return b;
 }
 
-/* ln u for u in (0, 1): u = m 2^e, m in [sqrt(1/2), sqrt(2)); ln m = t q(t), t = m - 1 (as awgn.hpp) */
-static float awgn_log(float u) {
-  const uint32_t b = f_bits(u);
-  int e = (int)((b >> 23) & 0xffu) - 127;
-  float m = f_from_bits((b & 0x007fffffu) | 0x3f800000u);
-  if (m > 1.41421354f) {
-    m = m * 0.5f;
-    e += 1;
-  }
-  /* ln m = t q(t), t = m - 1 in [sqrt(1/2) - 1, sqrt(2) - 1]: degree-8 q fitted on Chebyshev nodes,
-     max abs error 4.8e-8 in float32 Horner evaluation (no division) */
-  const float t = m - 1.0f;
-  float p = 0.08743945509195328f;
-  p = fmaf(p, t, -0.14377330243587494f);
-  p = fmaf(p, t, 0.14949095249176025f);
-  p = fmaf(p, t, -0.16560696065425873f);
-  p = fmaf(p, t, 0.19956977665424347f);
-  p = fmaf(p, t, -0.2500215470790863f);
-  p = fmaf(p, t, 0.3333418369293213f);
-  p = fmaf(p, t, -0.49999988079071045f);
-  p = fmaf(p, t, 1.0f);
-  const float lnm = p * t;
-  const float fe = (float)e;
-  return fmaf(fe, 0.693145751953125f, fmaf(fe, 1.428606765330187e-06f, lnm));
+/* The half-normal quantile table (R, S) of awgn.hpp, the same generated file the device reads
+ * (tools/make_awgn_table.py): the table is part of the construction's definition, like Philox's
+ * constants. tests/test_oracle_awgn.py checks the normals against float64 ndtri of the same bits. */
+static const float awgn_table[21 * 32][2] = {
+#define GSDR_AWGN_ENTRY(r, s) {r, s},
+#include "../gsdr_amd/csrc/awgn_table.inc"
+#undef GSDR_AWGN_ENTRY
+};
+
+/* One standard normal from 21 random bits (gsdr_amd/csrc/awgn.hpp awgn_normal): sign = bit 20,
+ * v = (2a + 1) 2^-21, |g| = fmaf(S, f, R) at index = exponent and top 5 mantissa bits of (float)(2a + 1),
+ * f = its other 18 mantissa bits * 2^-18 (exact). */
+float oracle_awgn_normal21(uint32_t r) {
+  const uint32_t x = ((r & 0xfffffu) << 1) | 1u;
+  const uint32_t b = f_bits((float)x);
+  const uint32_t i = (b >> 18) - 127u * 32u;
+  const float f = (float)(b & 0x3ffffu) * 3.814697265625e-06f;      /* 2^-18, exact */
+  const float m = fmaf(awgn_table[i][1] * 262144.0f, f, awgn_table[i][0]); /* the table's S 2^-18, times 2^18 */
+  return f_from_bits(f_bits(m) ^ ((r << 11) & 0x80000000u));
 }
 
-/* (cos, sin)(2 pi u) for u in [0, 1): quadrant q = floor(4u), f = 4u - q (both exact), polynomials in f
- * for the angle f pi / 2 */
-static void awgn_sincos_turns(float u, float* c, float* s) {
-  const float u4 = u * 4.0f;
-  const int q = (int)u4;
-  const float f = u4 - (float)q;
-  const float z = f * f;
-  float sp = 5.6921727775716136e-08f;
-  sp = fmaf(sp, z, -3.598843250074424e-06f);
-  sp = fmaf(sp, z, 0.00016044118092395365f);
-  sp = fmaf(sp, z, -0.004681753925979137f);
-  sp = fmaf(sp, z, 0.07969262450933456f);
-  sp = fmaf(sp, z, -0.6459640860557556f);
-  sp = fmaf(sp, z, 1.5707963705062866f);
-  const float sn = sp * f;
-  float cp = -6.386603246255618e-09f;
-  cp = fmaf(cp, z, 4.710874748070637e-07f);
-  cp = fmaf(cp, z, -2.520204179745633e-05f);
-  cp = fmaf(cp, z, 0.0009192602592520416f);
-  cp = fmaf(cp, z, -0.020863480865955353f);
-  cp = fmaf(cp, z, 0.25366950035095215f);
-  cp = fmaf(cp, z, -1.2337005138397217f);
-  const float cs = fmaf(cp, z, 1.0f);
-  switch (q & 3) {
-    case 0: *c = cs; *s = sn; break;
-    case 1: *c = -sn; *s = cs; break;
-    case 2: *c = -cs; *s = -sn; break;
-    default: *c = sn; *s = -cs; break;
-  }
-}
-
-static void awgn_box_muller(uint32_t a, uint32_t b, float* g0, float* g1) {
-  const float u1 = ((float)a + 0.5f) * 1.1920928955078125e-07f; /* 2^-23 */
-  const float u2 = (float)b * 1.52587890625e-05f;               /* 2^-16 */
-  const float r = sqrtf(-2.0f * awgn_log(u1));
-  float c, s;
-  awgn_sincos_turns(u2, &c, &s);
-  *g0 = r * c;
-  *g1 = r * s;
-}
-
-/* symbol k: Philox block k / 3 (counter (blk lo, blk hi, 0, 0), key = seed), slot k % 3, 39 bits a slot
- * (gsdr_amd/csrc/awgn.hpp) */
+/* symbol k: Philox block k / 3 (counter (blk lo, blk hi, 0, 0), key = seed), slot k % 3, 21 bits a
+ * component (gsdr_amd/csrc/awgn.hpp) */
 void oracle_awgn_normals(uint64_t seed, uint64_t symbol_index, float* g0, float* g1) {
   const uint64_t blk = symbol_index / 3u;
   const uint32_t ctr[4] = {(uint32_t)blk, (uint32_t)(blk >> 32), 0u, 0u};
@@ -565,9 +519,12 @@ void oracle_awgn_normals(uint64_t seed, uint64_t symbol_index, float* g0, float*
   uint32_t w[4];
   oracle_philox4x32_10(ctr, key, w);
   switch ((int)(symbol_index % 3u)) {
-    case 0: awgn_box_muller(w[0] >> 9, w[3] & 0xffffu, g0, g1); break;
-    case 1: awgn_box_muller(w[1] >> 9, w[3] >> 16, g0, g1); break;
-    default: awgn_box_muller(w[2] >> 9, ((w[0] & 0x1ffu) << 7) | (w[1] & 0x7fu), g0, g1); break;
+    case 0: *g0 = oracle_awgn_normal21(w[0] >> 11); *g1 = oracle_awgn_normal21(w[1] >> 11); break;
+    case 1: *g0 = oracle_awgn_normal21(w[2] >> 11); *g1 = oracle_awgn_normal21(w[3] >> 11); break;
+    default:
+      *g0 = oracle_awgn_normal21(((w[0] & 0x7ffu) << 10) | ((w[1] & 0x7ffu) >> 1));
+      *g1 = oracle_awgn_normal21(((w[2] & 0x7ffu) << 10) | ((w[3] & 0x7ffu) >> 1));
+      break;
   }
 }
 

@@ -110,14 +110,14 @@ void oracle_qpsk256_demod_cuabs(const float* table, const float* in, uint8_t* ou
 
 /* Config 5's channel (gsdrxQpsk256ModulateAwgn, include/gsdr/gsdr_ext.h): counter-based AWGN that the
  * host reproduces bit for bit. Philox4x32-10 (Salmon et al., SC'11) keyed by the 64-bit seed, counter
- * = (block lo, hi, 0, 0) with block = absolute symbol index / 3; slot k % 3 takes 23 bits a and 16 bits
- * b of the block's words w0..w3 (slot 0: w0 >> 9, w3 & 0xffff; slot 1: w1 >> 9, w3 >> 16; slot 2:
- * w2 >> 9, (w0 & 0x1ff) << 7 | (w1 & 0x7f)); u1 = (a + 0.5) 2^-23 in (0, 1), u2 = b 2^-16 in [0, 1);
- * (g0, g1) = sqrt(-2 ln u1) (cos, sin)(2 pi u2) by Box-Muller, with ln, sin and cos
- * evaluated by fixed polynomial sequences of IEEE +, -, *, sqrt and fmaf only (no libm), so the
- * device and the host round identically. Output = table[s] + (sigma g0, sigma g1), each sum rounded
- * once. */
+ * = (block lo, hi, 0, 0) with block = absolute symbol index / 3; slot k % 3 takes 21 bits a component
+ * from the block's words w0..w3 (slot 0: w0 >> 11, w1 >> 11; slot 1: w2 >> 11, w3 >> 11; slot 2:
+ * (w0 & 0x7ff) << 10 | (w1 & 0x7ff) >> 1, (w2 & 0x7ff) << 10 | (w3 & 0x7ff) >> 1). A component's bits
+ * give a sign and the tail probability v = (2a + 1) 2^-21; |g| is the half-normal quantile -Phi^-1(v/2)
+ * by linear interpolation in a 21 x 32 table (gsdr_amd/csrc/awgn_table.inc; one fmaf), so the device
+ * and the host round identically. Output = fl(table[s] + fl(sigma g)) per component (no FMA). */
 void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+float oracle_awgn_normal21(uint32_t r);
 void oracle_awgn_normals(uint64_t seed, uint64_t symbol_index, float* g0, float* g1);
 void oracle_qpsk256_mod_awgn(const float* table, const uint8_t* in, float* out, uint32_t n, float sigma,
                              uint64_t seed, uint64_t first_symbol);

@@ -64,6 +64,8 @@ for _name, _args in _SIG.items():
 _lib.oracle_nco_inc.argtypes = [_f, _f, _f]
 _lib.oracle_cuCabsf.argtypes = [_f, _f]
 _lib.oracle_cuCabsf.restype = _f
+_lib.oracle_awgn_normal21.argtypes = [_u32]
+_lib.oracle_awgn_normal21.restype = _f
 _lib.oracle_nco_inc.restype = _u32
 
 
@@ -238,6 +240,11 @@ def philox4x32_10(ctr, key):
     out = np.empty(4, dtype=np.uint32)
     _lib.oracle_philox4x32_10(_ptr(c), _ptr(k), _ptr(out))
     return out
+
+
+def awgn_normal21(bits):
+    """One standard normal from 21 random bits (the AWGN construction, gsdr_amd/csrc/awgn.hpp)."""
+    return float(_lib.oracle_awgn_normal21(bits))
 
 
 def awgn_normals(seed, symbol_index):

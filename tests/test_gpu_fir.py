@@ -45,7 +45,7 @@ def run_fir(cuda, taps, x, D, N, x_offset=0):
 
 
 @pytest.mark.parametrize("T", [1, 8, 63, 127, 200])
-@pytest.mark.parametrize("D", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 12, 13, 16, 20, 24, 32, 40, 50, 64])
+@pytest.mark.parametrize("D", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 12, 13, 16, 20, 24, 32, 40, 50, 64, 100])
 @pytest.mark.parametrize("tt", list(TYPES))
 def test_fir_parity(cuda, tt, D, T):
     N = 2 * 4096 + 37  # several tiles plus a ragged tail

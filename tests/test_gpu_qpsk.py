@@ -212,6 +212,24 @@ def test_qpsk256_awgn_sizes_and_offsets(cuda, n, first):
         assert np.concatenate([a, b]).tobytes() == rx.tobytes()
 
 
+@pytest.mark.parametrize("in_off,out_off", [(0, 0), (1, 0), (0, 1), (1, 1), (2, 1)])
+def test_qpsk256_awgn_pointer_alignment(cuda, in_off, out_off):
+    """Odd input bytes and an output 8 bytes off 16-byte alignment take the per-lane path; aligned
+    pointers the wave's LDS-transposed stores. Same bits either way, whole and ragged waves."""
+    from gsdr_amd import ops
+
+    ctype, sigma, seed, first = 0, 0.02, 0x5EED0005, 7
+    ops.qpsk256_init(ctype, 1.0)
+    table = o.qpsk256_table(ctype, 1.0)
+    n = 3 * 4608 + 385
+    syms_np = np.random.default_rng(in_off * 7 + out_off).integers(0, 256, n + 4, dtype=np.uint8)
+    syms = dev(syms_np, cuda)[in_off:in_off + n]
+    out = torch.empty(n + 1, dtype=torch.complex64, device=cuda)[out_off:out_off + n]
+    ops.qpsk256_modulate_awgn(syms, ctype, sigma, seed, first, out=out)
+    want = o.qpsk256_mod_awgn(table, syms_np[in_off:in_off + n], sigma, seed, first)
+    assert out.cpu().numpy().tobytes() == want.tobytes()
+
+
 def test_qpsk256_awgn_zero_sigma_is_modulate(cuda):
     from gsdr_amd import GsdrError, ops
 

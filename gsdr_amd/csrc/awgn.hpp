@@ -44,7 +44,10 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t k) {
 __device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
                                               uint32_t k1, uint32_t (&w)[4]) {
 #pragma unroll
-  for (int r = 0; r < 10; ++r) {
+#ifndef GSDR_PHILOX_ROUNDS
+#define GSDR_PHILOX_ROUNDS 10
+#endif
+  for (int r = 0; r < GSDR_PHILOX_ROUNDS; ++r) {
     // one 32 x 32 -> 64-bit product per multiplier (v_mad_u64_u32) instead of separate mul_lo / mul_hi:
     // both are quarter-rate, and these 40 products per three symbols bound the kernel
     const uint64_t p0 = (uint64_t)c0 * 0xD2511F53u, p1 = (uint64_t)c2 * 0xCD9E8D57u;

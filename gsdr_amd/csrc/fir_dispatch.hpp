@@ -92,7 +92,24 @@ inline bool shifted_staging(const void* in, uint64_t samples_per_tile) {
     // int8 I/Q one sample (2 bytes) off 4-byte alignment: shifted 4-byte word loads
     return (reinterpret_cast<uintptr_t>(in) % 4) == 2 && samples_per_tile % 2 == 0;
   } else {
-    return false;
+    // real samples 1..3 floats off 16-byte alignment (stage_tile's real SH mode, SH = the offset)
+    return (reinterpret_cast<uintptr_t>(in) % 4) == 0 && (reinterpret_cast<uintptr_t>(in) % 16) != 0 &&
+           samples_per_tile % 4 == 0;
+  }
+}
+
+// Launch kernel template K<SH> with the shift the input pointer needs (shifted_staging is true): 1 for
+// complex / int8 I/Q input, the float offset 1..3 for real input.
+template <class InT, class F>
+inline void launch_shifted(const void* in, F&& f) {
+  if constexpr (std::is_same<InT, float>::value) {
+    switch ((reinterpret_cast<uintptr_t>(in) % 16) / 4) {
+      case 1: f(std::integral_constant<int, 1>{}); break;
+      case 2: f(std::integral_constant<int, 2>{}); break;
+      default: f(std::integral_constant<int, 3>{}); break;
+    }
+  } else {
+    f(std::integral_constant<int, 1>{});
   }
 }
 
@@ -126,10 +143,10 @@ hipError_t launch_poly(const FirJob& j, hipStream_t s) {
   if (vec) {
     k_fir_poly<TapT, InT, D, R, JC, WG, true, MODE, ABL, NT, XM, CST, DMA><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
   } else if (shifted_staging<InT>(j.in, (uint64_t)stride * D)) {
-    if constexpr (std::is_same<InT, float2>::value || std::is_same<InT, Iq8>::value) {
-      k_fir_poly<TapT, InT, D, R, JC, WG, false, MODE, ABL, NT, XM, CST, false, true>
+    launch_shifted<InT>(j.in, [&](auto sh) {
+      k_fir_poly<TapT, InT, D, R, JC, WG, false, MODE, ABL, NT, XM, CST, false, decltype(sh)::value>
           <<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
-    }
+    });
   } else {
     k_fir_poly<TapT, InT, D, R, JC, WG, false, MODE, ABL, NT, XM, CST, DMA><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
   }
@@ -173,9 +190,10 @@ hipError_t launch_contig(const FirJob& j, hipStream_t s) {
   if (vec) {
     k_fir_contig<TapT, InT, D, R, IC, WG, true, MODE><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
   } else if (shifted_staging<InT>(j.in, (uint64_t)stride * D)) {
-    if constexpr (std::is_same<InT, float2>::value || std::is_same<InT, Iq8>::value) {
-      k_fir_contig<TapT, InT, D, R, IC, WG, false, MODE, true><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
-    }
+    launch_shifted<InT>(j.in, [&](auto sh) {
+      k_fir_contig<TapT, InT, D, R, IC, WG, false, MODE, decltype(sh)::value>
+          <<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
+    });
   } else {
     k_fir_contig<TapT, InT, D, R, IC, WG, false, MODE><<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
   }

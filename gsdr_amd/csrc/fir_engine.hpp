@@ -398,7 +398,7 @@ __device__ __forceinline__ bool stage_body_dma(float4* __restrict__ lds, const I
 // split over two LDS granules (second half of slot g - 1, first half of slot g); the halo re-writes the
 // body's last slot whole. The NCO phasor is a function of the absolute index, so the odd-start pairs
 // mix exactly as the even-start ones would.
-template <class InT, class Geo, int WG, bool VEC, int MODE, bool NT = false, bool DMA = false, bool SH = false,
+template <class InT, class Geo, int WG, bool VEC, int MODE, bool NT = false, bool DMA = false, int SH = 0,
           bool NODIRECT = false>
 __device__ __forceinline__ void stage_tile(float4* __restrict__ lds, const InT* __restrict__ in, uint64_t S0,
                                            uint32_t NG, const FirParams& p) {
@@ -413,8 +413,49 @@ __device__ __forceinline__ void stage_tile(float4* __restrict__ lds, const InT* 
   const PhaseWalk pw = phase_walk<G, WG>(p.nco_n0, S0, p.nco_inc);
   // wave-uniform: is the whole staged span readable? (every tile but the last)
   const bool whole = VEC && (S0 + (uint64_t)NG * G <= p.L);
-  if constexpr (SH) {
-    static_assert((std::is_same<InT, float2>::value || std::is_same<InT, Iq8>::value) && !VEC,
+  if constexpr (SH != 0 && std::is_same<InT, float>::value) {
+    // real samples SH (1..3) floats off 16-byte alignment (4-byte aligned): aligned 16-byte loads from
+    // SH samples early; loaded quad g holds the last SH samples of granule g - 1 and the first 4 - SH of
+    // granule g, written as two partial-granule LDS stores (8-byte aligned pieces). The halo re-writes
+    // the body's last granule whole, as for complex input.
+    static_assert(!VEC && SH > 0 && SH < 4, "shifted real staging: 1..3 floats off 16-byte alignment");
+    if (S0 + (uint64_t)NG * G <= p.L) {
+      float* __restrict__ l1 = reinterpret_cast<float*>(lds);
+      const float4* __restrict__ src = reinterpret_cast<const float4*>(in + S0 - SH);  // 16-byte aligned
+#pragma unroll
+      for (int b0 = 0; b0 < BPT; b0 += SB) {
+        float4 v[SB];
+#pragma unroll
+        for (int k = 0; k < SB; ++k) v[k] = NT ? load16_nt(src + (b0 + k) * WG + tid) : src[(b0 + k) * WG + tid];
+#pragma unroll
+        for (int k = 0; k < SB; ++k) {
+          const uint32_t g = (b0 + k) * WG + tid;
+          float* __restrict__ lo = l1 + 4 * Geo::padded(g);  // granule g
+          if constexpr (SH == 2) {
+            if (g > 0) *reinterpret_cast<float2*>(l1 + 4 * Geo::padded(g - 1) + 2) = make_float2(v[k].x, v[k].y);
+            *reinterpret_cast<float2*>(lo) = make_float2(v[k].z, v[k].w);
+          } else if constexpr (SH == 1) {
+            if (g > 0) l1[4 * Geo::padded(g - 1) + 3] = v[k].x;
+            *reinterpret_cast<float2*>(lo) = make_float2(v[k].y, v[k].z);
+            lo[2] = v[k].w;
+          } else {
+            if (g > 0) {
+              float* __restrict__ pv = l1 + 4 * Geo::padded(g - 1);
+              pv[1] = v[k].x;
+              *reinterpret_cast<float2*>(pv + 2) = make_float2(v[k].y, v[k].z);
+            }
+            lo[0] = v[k].w;
+          }
+        }
+      }
+      for (uint32_t g = BPT * WG - 1 + tid; g < NG; g += WG) {
+        const uint64_t s = S0 + (uint64_t)g * G;
+        lds[Geo::padded(g)] = load_granule<InT, false>(in, s, p.L);
+      }
+      return;
+    }
+  } else if constexpr (SH != 0) {
+    static_assert((std::is_same<InT, float2>::value || std::is_same<InT, Iq8>::value) && !VEC && SH == 1,
                   "shifted staging is for 8-byte-aligned complex or 2-byte-aligned int8 I/Q input");
     if (S0 + (uint64_t)NG * G <= p.L) {
       float2* __restrict__ l2 = reinterpret_cast<float2*>(lds);
@@ -912,7 +953,7 @@ __device__ __forceinline__ uint32_t tile_of_block() {
 
 // One tile of the polyphase kernel (the body of k_fir_poly and of k_fir_poly_grouped).
 template <class TapT, class InT, int D, int R, int JC, int WG, bool VEC, int MODE, int ABL, bool NT, int CST, bool DMA,
-          bool SH>
+          int SH>
 __device__ __forceinline__ void fir_poly_tile(const FirParams& p, uint32_t tile) {
   using Geo = TileGeo<InT, D, R, WG>;
   using OutT = typename Product<TapT, InT>::type;
@@ -961,7 +1002,7 @@ __device__ __forceinline__ void fir_poly_tile(const FirParams& p, uint32_t tile)
 }
 
 template <class TapT, class InT, int D, int R, int JC, int WG, bool VEC, int MODE, int ABL = 0, bool NT = false,
-          bool XM = false, int CST = 0, bool DMA = false, bool SH = false>
+          bool XM = false, int CST = 0, bool DMA = false, int SH = 0>
 __global__ __launch_bounds__(WG) void k_fir_poly(FirParams p) {
   fir_poly_tile<TapT, InT, D, R, JC, WG, VEC, MODE, ABL, NT, CST, DMA, SH>(p, tile_of_block<XM>());
 }
@@ -986,7 +1027,7 @@ struct MultiParams {
 // channel c is bit-identical to gsdrFmDemod / gsdrAmDemod with its own frequency by construction, at
 // the single-channel kernel's register budget. (The first multi-channel kernel read each input tile
 // into registers once and looped over the channels: 228 VGPRs, 2 waves per SIMD, 5 % slower.)
-template <class TapT, class InT, int D, int R, int JC, int WG, bool VEC, int MODE, bool SH = false>
+template <class TapT, class InT, int D, int R, int JC, int WG, bool VEC, int MODE, int SH = 0>
 __global__ __launch_bounds__(WG) void k_fir_poly_grouped(FirParams p, MultiParams mp, uint32_t tiles) {
   const uint32_t C = mp.count;
   const uint32_t b = blockIdx.x, r = b >> 3;
@@ -1003,7 +1044,7 @@ __global__ __launch_bounds__(WG) void k_fir_poly_grouped(FirParams p, MultiParam
 // Kernel 2: contiguous-window kernel for small D (D = 1 in particular).
 //   IC = taps per chunk (a multiple of R*D).
 // ------------------------------------------------------------------------------------------------
-template <class TapT, class InT, int D, int R, int IC, int WG, bool VEC, int MODE, bool SH = false>
+template <class TapT, class InT, int D, int R, int IC, int WG, bool VEC, int MODE, int SH = 0>
 __global__ __launch_bounds__(WG) void k_fir_contig(FirParams p) {
   using Geo = TileGeo<InT, D, R, WG>;
   using OutT = typename Product<TapT, InT>::type;

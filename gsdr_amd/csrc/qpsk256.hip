@@ -234,7 +234,10 @@ __global__ __launch_bounds__(kCBlock) void k_c256_mod(C256Streams st, uint32_t n
 // (48-byte lane stride) they ran at about half the copy rate, which bound the kernel once the normals
 // were cheap (the write-heavy maps of section 3.6 showed the same).
 constexpr int kAwgnSym = 6;    // symbols per lane per step
-constexpr int kAwgnSteps = 3;  // steps per workgroup
+#ifndef GSDR_AWGN_STEPS
+#define GSDR_AWGN_STEPS 3
+#endif
+constexpr int kAwgnSteps = GSDR_AWGN_STEPS;  // steps per workgroup
 constexpr uint32_t kAwgnWaveSyms = 64u * kAwgnSym;
 constexpr uint32_t kAwgnBlockSyms = kCBlock * kAwgnSym * kAwgnSteps;
 

@@ -284,3 +284,19 @@ def test_fir_shifted_staging_bit_identical(cuda, tt, D):
     aligned = run_fir(cuda, taps, x, D, N)
     shifted = run_fir(cuda, taps, x, D, N, x_offset=1)
     assert aligned.tobytes() == shifted.tobytes()
+
+
+@pytest.mark.parametrize("off", [1, 2, 3])
+@pytest.mark.parametrize("tt,D", [("FF", 4), ("FF", 1), ("FF", 8), ("CF", 4), ("CF", 1), ("FF", 12), ("CF", 16),
+                                  ("FF", 20)])
+def test_fir_shifted_real_staging_bit_identical(cuda, tt, D, off):
+    """Real input 1..3 floats off 16-byte alignment is staged with aligned 16-byte loads from `off`
+    samples early, each quad split over two LDS granules (stage_tile's real SH mode); the outputs equal
+    those of the same samples at an aligned address bit for bit, and the oracle's within the bar."""
+    N, T = 3 * 4096 + 5, 127
+    L = (N - 1) * D + T
+    taps, x = make(tt, T, L, seed=17 * off + D)
+    aligned = run_fir(cuda, taps, x, D, N)
+    shifted = run_fir(cuda, taps, x, D, N, x_offset=off)
+    assert aligned.tobytes() == shifted.tobytes()
+    assert normwise_err(shifted, o.fir(taps, x, D, N), bound(taps, x, D, N)) <= FLOAT_TOL

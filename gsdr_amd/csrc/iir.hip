@@ -223,6 +223,15 @@ constexpr bool kTableInLds = kGroup * P * P * sizeof(double) <= 32 * 1024;
 #define IIR_FUSED_MAXP 8
 #endif
 constexpr int kFusedMaxP = IIR_FUSED_MAXP;
+// Ablation probes for timing only (wrong results; never set in the product build): IIR_PROBE_TAILS bits
+// 1 = no transition powers, 2 = no level-0 up-sweep, 4 = no recursion in the tails pass; IIR_PROBE_FINAL
+// bits 1 = no start-state prologue, 2 = no recursion in the final pass.
+#ifndef IIR_PROBE_TAILS
+#define IIR_PROBE_TAILS 0
+#endif
+#ifndef IIR_PROBE_FINAL
+#define IIR_PROBE_FINAL 0
+#endif
 
 struct ScanArgs {
   double* incl;          // level-0 inclusive zero-state prefixes (A[P] per chunk); tails pass writes
@@ -230,11 +239,6 @@ struct ScanArgs {
   const double* T0;      // M_0^r, r < 64 (final pass)
   const double* gstart;  // level-1 start states (final pass), or null: s0 is the group start
   const double* s0;
-  // level-1 down-sweep folded into the final pass (levels >= 2): the level-1 inclusive prefixes, M_1^r
-  // and the level-2 start states; then gstart is unused
-  const double* incl1;
-  const double* T1;
-  const double* gstart2;
 };
 
 // Up-sweep of one level-0 group from the workgroup's tails in LDS (loc = the group's 64 elements),
@@ -359,54 +363,49 @@ __global__ __launch_bounds__(TileShape<S>::WG) void k_iir_chunks(Coeffs cf, cons
     const uint64_t base = ti * TSh::TS;
     const uint32_t tlen = n - base < (uint64_t)TSh::TS ? (uint32_t)(n - base) : (uint32_t)TSh::TS;
     const bool whole = is_whole(ti);
+    const uint64_t c = ti * TSh::CPW + t / NC;
+    const uint64_t n0 = c * kChunk;
+    double ys[P];  // component of y[n-1-i]: the chunk's start state
+#pragma unroll
+    for (int i = 0; i < P; ++i) ys[i] = 0.0;
+    // Final pass: the operands of the chunk's start state are loaded BEFORE the tile. Vector loads retire
+    // in order, so operands loaded after the tile could only be used once the whole tile had arrived: the
+    // start state's FMAs would then sit on the critical path instead of under the tile's load latency.
+    constexpr bool kPro = FUSED && PASS == kFinal && !(IIR_PROBE_FINAL & 1);
+    constexpr int PP = P * P;
+    double mr[kPro ? PP : 1], inc[kPro ? P : 1], sgc[kPro ? P : 1];
+    const uint64_t g = c / kGroup;
+    const int r = (int)(c % kGroup);
+    if constexpr (kPro) {
+      // level-0 down-sweep for this chunk: start = M_0^r S_g + prefix_(r-1) (as down_group)
+      if (n0 < n) {
+        const double* __restrict__ Mr = sc.T0 + (size_t)r * PP;
+#pragma unroll
+        for (int e = 0; e < PP; ++e) mr[e] = Mr[e];
+#pragma unroll
+        for (int i = 0; i < P; ++i) inc[i] = r > 0 ? sc.incl[((c - 1) * P + i) * NC + comp] : 0.0;
+        const double* __restrict__ sg = sc.gstart ? sc.gstart + g * P * NC : sc.s0;
+#pragma unroll
+        for (int l = 0; l < P; ++l) sgc[l] = sg[l * NC + comp];
+      }
+    }
     float4 v[NV];
     if (whole) load_tile(ti, v);  // in flight while the final pass computes the chunk start state
 
     // the P samples before the tile (the input history for the first tile), loaded beside it
     S pv = zero_s(S{});
     if (t < P) pv = x_at(x, xh, cf.K, (int64_t)base - 1 - t);
-    const uint64_t c = ti * TSh::CPW + t / NC;
-    const uint64_t n0 = c * kChunk;
-    double ys[P];  // component of y[n-1-i]: the chunk's start state
-#pragma unroll
-    for (int i = 0; i < P; ++i) ys[i] = 0.0;
-    if constexpr (FUSED && PASS == kFinal) {
-      // level-0 down-sweep for this chunk: start = M_0^r S_g + prefix_(r-1) (as down_group)
+    if constexpr (kPro) {
       if (n0 < n) {
-        const uint64_t g = c / kGroup;
-        const int r = (int)(c % kGroup);
-        const double* __restrict__ Mr = sc.T0 + (size_t)r * P * P;
-        double sgc[P];
-        if (sc.incl1) {
-          // the group's start = level-1 element g's start, M_1^r1 S_(g / 64) + prefix1_(g - 1) (as
-          // down_group), in place of a level-1 down-sweep launch
-          const uint64_t g2 = g / kGroup;
-          const int r1 = (int)(g % kGroup);
-          const double* __restrict__ M1 = sc.T1 + (size_t)r1 * P * P;
-          double s2[P];
-#pragma unroll
-          for (int l = 0; l < P; ++l) s2[l] = sc.gstart2[(g2 * P + l) * NC + comp];
-#pragma unroll
-          for (int i = 0; i < P; ++i) {
-            double acc = r1 > 0 ? sc.incl1[((g - 1) * P + i) * NC + comp] : 0.0;
-#pragma unroll
-            for (int l = 0; l < P; ++l) acc = fma(M1[i * P + l], s2[l], acc);
-            sgc[i] = acc;
-          }
-        } else {
-          const double* __restrict__ sg = sc.gstart ? sc.gstart + g * P * NC : sc.s0;
-#pragma unroll
-          for (int l = 0; l < P; ++l) sgc[l] = sg[l * NC + comp];
-        }
 #pragma unroll
         for (int i = 0; i < P; ++i) {
-          double acc = r > 0 ? sc.incl[((c - 1) * P + i) * NC + comp] : 0.0;
+          double acc = inc[i];
 #pragma unroll
-          for (int l = 0; l < P; ++l) acc = fma(Mr[i * P + l], sgc[l], acc);
+          for (int l = 0; l < P; ++l) acc = fma(mr[i * P + l], sgc[l], acc);
           ys[i] = acc;
         }
       }
-    } else if constexpr (PASS == kFinal) {
+    } else if constexpr (PASS == kFinal && !FUSED) {
       if (n0 < n) {
         const double* __restrict__ starts_d = reinterpret_cast<const double*>(starts);
 #pragma unroll
@@ -465,7 +464,8 @@ __global__ __launch_bounds__(TileShape<S>::WG) void k_iir_chunks(Coeffs cf, cons
         ys[0] = acc;
         if constexpr (PASS == kFinal) row[k * NC] = (float)acc;  // y replaces x in this chunk's row
       };
-      if (len == (uint32_t)kChunk) {
+      if ((PASS == kTails && (IIR_PROBE_TAILS & 4)) || (PASS == kFinal && (IIR_PROBE_FINAL & 2))) {
+      } else if (len == (uint32_t)kChunk) {
 #pragma unroll
         for (uint32_t k = 0; k < (uint32_t)kChunk; ++k) step(k);
       } else {
@@ -487,7 +487,7 @@ __global__ __launch_bounds__(TileShape<S>::WG) void k_iir_chunks(Coeffs cf, cons
       }
     }
     if constexpr (PASS == kTails && FUSED) {
-      if (ti == first_ti) build_pow();
+      if (!(IIR_PROBE_TAILS & 1) && ti == first_ti) build_pow();
       lds_barrier();  // every lane is done reading the tile
       if (n0 < n) {
 #pragma unroll
@@ -495,7 +495,7 @@ __global__ __launch_bounds__(TileShape<S>::WG) void k_iir_chunks(Coeffs cf, cons
       }
       lds_barrier();
       const int w = t / kGroup;
-      if (w < TSh::CPW / kGroup) {
+      if (!(IIR_PROBE_TAILS & 2) && w < TSh::CPW / kGroup) {
         const uint64_t C = (n + kChunk - 1) / kChunk;
         const uint64_t g = ti * (TSh::CPW / kGroup) + w;
         up_group_fused<A, P>(tl + w * kGroup * P, C, mpow, reinterpret_cast<A*>(sc.incl),
@@ -636,6 +636,111 @@ __global__ __launch_bounds__(64 * kRestWaves) void k_iir_scan_rest(Levels<A> L, 
   }
 }
 
+// Levels >= 2 up and down plus level 1's down-sweep in ONE launch (E2 <= kUpperE2 level-2 elements:
+// 2^25 samples), after level 1's up-sweep (k_iir_up). Every workgroup scans all of level 2 itself (at most 4
+// groups of 64, one wave each, in registers and LDS: a few KB from L2) and derives the level-2 start states
+// its own level-1 groups need; then wave j down-sweeps level-1 group 4 b + j of its workgroup b. The
+// redundant upper scan costs nothing next to what it replaces: the single-workgroup upper-level kernel
+// walked levels 2..3 through global memory (one dependent round trip per phase, 8.3 us at 2^24 samples) and
+// a separate level-1 down-sweep (or its fold into the final pass's prologue).
+constexpr int kUpperWaves = 4;
+constexpr uint64_t kUpperE2 = kUpperWaves * kGroup;
+
+template <int P>
+__device__ __forceinline__ void mat_vec_acc(const double* __restrict__ M, const double (&x)[P], double (&acc)[P]) {
+#pragma unroll
+  for (int i = 0; i < P; ++i) {
+    double a = acc[i];
+#pragma unroll
+    for (int l = 0; l < P; ++l) a = fma(M[i * P + l], x[l], a);
+    acc[i] = a;
+  }
+}
+
+// T[k] = M_k^r, r < 64 (setup tables); elems1 = level-1 elements (their inclusive prefixes in starts1 from
+// k_iir_up, overwritten with start states), elems2 = level-2 elements (group aggregates of level 1)
+template <int P>
+__global__ __launch_bounds__(64 * kUpperWaves) void k_iir_scan_upper(uint64_t E1, uint64_t E2, int NC,
+                                                                     const double* __restrict__ T1,
+                                                                     const double* __restrict__ T2,
+                                                                     const double* __restrict__ T3,
+                                                                     const double* __restrict__ elems2,
+                                                                     const double* __restrict__ s0,
+                                                                     double* __restrict__ starts1) {
+  constexpr int PP = P * P;
+  __shared__ double incl2[kUpperE2][P];      // level-2 zero-state inclusive prefixes within their group
+  __shared__ double gstart[kUpperWaves][P];  // level-2 group start states
+  const int comp = blockIdx.y;
+  const int t = threadIdx.x, r = t % 64, w = t / 64;
+  // this wave's level-1 group (= level-2 element) and its own operands, loaded first
+  const uint64_t e2 = (uint64_t)blockIdx.x * kUpperWaves + w;
+  const uint64_t e1 = e2 * kGroup + r;
+  const bool live = e2 < E2 && e1 < E1;
+  double mine[P], m1r[PP];
+#pragma unroll
+  for (int i = 0; i < P; ++i) mine[i] = live ? starts1[(e1 * P + i) * NC + comp] : 0.0;
+#pragma unroll
+  for (int q = 0; q < PP; ++q) m1r[q] = T1[(size_t)r * PP + q];
+  // 1. level 2: every workgroup scans all E2 elements, wave j the group j (one element a lane)
+  double v[P];
+  const uint64_t j2 = (uint64_t)t;
+#pragma unroll
+  for (int i = 0; i < P; ++i) v[i] = j2 < E2 ? elems2[(j2 * P + i) * NC + comp] : 0.0;
+#pragma unroll
+  for (int s = 0; s < 6; ++s) {
+    const int d = 1 << s;
+    double u[P];
+#pragma unroll
+    for (int i = 0; i < P; ++i) u[i] = __shfl_up(v[i], d, 64);
+    if (r >= d) mat_vec_acc<P>(T2 + (size_t)d * PP, u, v);
+  }
+#pragma unroll
+  for (int i = 0; i < P; ++i) incl2[t][i] = v[i];
+  __syncthreads();
+  // 2. the level-2 groups' start states: at most 4, composed in order from s0 (M_3 = M_2^64)
+  if (t < P) {
+    double sg[P];
+#pragma unroll
+    for (int i = 0; i < P; ++i) sg[i] = s0[i * NC + comp];
+    const int ng = (int)((E2 + kGroup - 1) / kGroup);
+    for (int q = 0; q < kUpperWaves; ++q) {
+      gstart[q][t] = sg[t];
+      if (q + 1 < ng) {
+        double nv[P];
+#pragma unroll
+        for (int i = 0; i < P; ++i) nv[i] = incl2[q * kGroup + kGroup - 1][i];
+        mat_vec_acc<P>(T3 + PP, sg, nv);
+#pragma unroll
+        for (int i = 0; i < P; ++i) sg[i] = nv[i];
+      }
+    }
+  }
+  __syncthreads();
+  if (!(e2 < E2)) return;
+  // 3. this wave's level-2 element start: M_2^r2 S_group + incl2[e2 - 1] (uniform across the wave)
+  const int r2 = (int)(e2 % kGroup);
+  const int q2 = (int)(e2 / kGroup);
+  double s2[P], sg[P];
+#pragma unroll
+  for (int i = 0; i < P; ++i) {
+    s2[i] = r2 > 0 ? incl2[e2 - 1][i] : 0.0;
+    sg[i] = gstart[q2][i];
+  }
+  mat_vec_acc<P>(T2 + (size_t)r2 * PP, sg, s2);
+  // 4. level-1 down-sweep of group e2: element e1 starts in M_1^r S2 + incl1[e1 - 1]
+  double st[P];
+#pragma unroll
+  for (int i = 0; i < P; ++i) {
+    const double prev = __shfl_up(mine[i], 1, 64);
+    st[i] = r > 0 ? prev : 0.0;
+  }
+  mat_vec_acc<P>(m1r, s2, st);
+  if (live) {
+#pragma unroll
+    for (int i = 0; i < P; ++i) starts1[(e1 * P + i) * NC + comp] = st[i];
+  }
+}
+
 // The caller's history buffers after the call, from the state staged by the last chunk.
 template <class S>
 __global__ __launch_bounds__(64) void k_iir_history(S* __restrict__ xh, S* __restrict__ yh,
@@ -671,6 +776,10 @@ static hipError_t run(const Coeffs& cf, S* xh, S* yh, const S* x, S* y, uint64_t
     off[k][1] = bytes;
     bytes += E[k] * P * sizeof(A);
   }
+  constexpr bool F = P <= kFusedMaxP;
+  // levels >= 2 and level 1's down-sweep in one launch when level 2 fits (k_iir_scan_upper, which reads
+  // the powers of M_1, M_2, M_3 from the tables)
+  const bool upper = F && levels >= 2 && E[2] <= kUpperE2;
   const size_t off_m = bytes;
   bytes += (size_t)(levels + 1) * kGroup * P * P * sizeof(double);  // T[level][r] = M_level^r
   const size_t off_s0 = bytes;
@@ -694,7 +803,6 @@ static hipError_t run(const Coeffs& cf, S* xh, S* yh, const S* x, S* y, uint64_t
   const uint32_t blocks = (uint32_t)ntiles;
   const SetupArgs sa{yh, s0, table(0), levels};
   const bool vec = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15u) == 0;
-  constexpr bool F = P <= kFusedMaxP;
   // fused: the tails pass leaves level-0 inclusive prefixes in starts(0) and the group aggregates in
   // elems(1); the final pass finishes level 0 itself
   const ScanArgs up_args{reinterpret_cast<double*>(starts(0)), levels > 0 ? reinterpret_cast<double*>(elems(1)) : nullptr,
@@ -717,27 +825,28 @@ static hipError_t run(const Coeffs& cf, S* xh, S* yh, const S* x, S* y, uint64_t
   const int lowest = F ? 1 : 0;  // levels scanned outside the chunk passes
   int rest = lowest;             // first level handled by the single-workgroup kernels
   while (rest <= levels && ceil_div<uint64_t>(E[rest], kGroup) > (uint64_t)kRestGroups) ++rest;
-  // With the level-0 scan fused, the final pass also takes level 1's down-sweep (levels >= 2, level 1
-  // scanned by its own up-sweep launch): 2^24 samples in 4 launches (tails, level-1 up, levels 2-3,
-  // final) instead of 5.
-  const bool fold1 = F && levels >= 2 && rest >= 2;
-  for (int k = lowest; k < rest; ++k) {
+  const int stop = upper ? 2 : rest;  // with k_iir_scan_upper: level 1's up-sweep, then that kernel
+  for (int k = lowest; k < stop; ++k) {
     k_iir_up<A, P><<<(uint32_t)ceil_div<uint64_t>(E[k], kGroup), 64, 0, st>>>(elems(k), E[k], table(k), starts(k),
                                                                              elems(k + 1));
   }
-  if (rest <= levels) k_iir_scan_rest<A, P><<<1, 64 * kRestWaves, 0, st>>>(L, s0, rest);
-  for (int k = rest - 1; k >= (fold1 ? 2 : lowest); --k) {
+  if constexpr (F) {
+    if (upper) {
+      const dim3 grid((uint32_t)ceil_div<uint64_t>(E[2], kUpperWaves), TileShape<S>::NC);
+      k_iir_scan_upper<P><<<grid, 64 * kUpperWaves, 0, st>>>(
+          E[1], E[2], TileShape<S>::NC, table(1), table(2), levels >= 3 ? table(3) : nullptr,
+          reinterpret_cast<const double*>(elems(2)), reinterpret_cast<const double*>(s0),
+          reinterpret_cast<double*>(starts(1)));
+    }
+  }
+  if (!upper && rest <= levels) k_iir_scan_rest<A, P><<<1, 64 * kRestWaves, 0, st>>>(L, s0, rest);
+  for (int k = upper ? 0 : stop - 1; k >= lowest; --k) {
     k_iir_down<A, P><<<(uint32_t)ceil_div<uint64_t>(E[k], kGroup), 64, 0, st>>>(E[k], table(k), starts(k + 1),
                                                                                starts(k));
   }
-  const ScanArgs down_args{reinterpret_cast<double*>(starts(0)),
-                           nullptr,
-                           table(0),
+  const ScanArgs down_args{reinterpret_cast<double*>(starts(0)), nullptr, table(0),
                            levels > 0 ? reinterpret_cast<const double*>(starts(1)) : nullptr,
-                           reinterpret_cast<const double*>(s0),
-                           fold1 ? reinterpret_cast<const double*>(starts(1)) : nullptr,
-                           fold1 ? table(1) : nullptr,
-                           fold1 ? reinterpret_cast<const double*>(starts(2)) : nullptr};
+                           reinterpret_cast<const double*>(s0)};
   if (vec) {
     k_iir_chunks<S, P, kFinal, true, F><<<blocks, WG, 0, st>>>(cf, x, xh, n, starts(0), st_out, y, SetupArgs{},
                                                                down_args);

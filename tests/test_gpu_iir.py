@@ -41,7 +41,7 @@ def err(got, want):
     return float(np.max(np.abs(got - want))) / max(1.0, float(np.max(np.abs(want))))
 
 
-SIZES = [1, 2, 5, 127, 128, 129, 1000, 8192, 8193, 128 * 64 + 1, 128 * 64 * 64 + 7, (1 << 22) + 3]
+SIZES = [1, 2, 5, 127, 128, 129, 1000, 8192, 8193, 128 * 64 + 1, 128 * 64 * 64 + 7, (1 << 22) + 3, 1 << 24]
 
 
 @pytest.mark.parametrize("n", SIZES)
@@ -142,3 +142,24 @@ def test_iir_impulse_and_validation(cuda):
                                    0, cuda.index, st) != 0
     assert abi.lib.gsdrIirFFCustom(bd.data_ptr(), bd.data_ptr(), 3, None, None, xd.data_ptr(), yd.data_ptr(), 0,
                                    8, cuda.index, st) == 0
+
+
+@pytest.mark.parametrize("order,n", [(4, 1 << 25), (4, (1 << 25) + 1), (8, (1 << 21) + 3), (2, (1 << 22) + 9),
+                                     (1, 3 * (1 << 21) + 1), (6, 64 * 64 * 32 * 3 + 5)])
+def test_iir_scan_paths(cuda, order, n):
+    """Levels >= 2 and level 1's down-sweep run in one launch (k_iir_scan_upper) up to 256 level-2
+    elements (2^25 samples); past that, the per-level launches. Inputs at and past the limit, partial
+    groups at every level, and a level-2 scan of one group (levels == 2), each against the float64
+    oracle with history."""
+    from gsdr_amd import ops
+
+    b, a = design("poles", order)
+    rng = np.random.default_rng(n)
+    x = rng.uniform(-1, 1, n).astype(np.float32)
+    xh = rng.uniform(-1, 1, order).astype(np.float32)
+    yh = rng.uniform(-1, 1, order).astype(np.float32)
+    y = ops.iir(dev(b, cuda), dev(a, cuda), dev(x, cuda), dev(xh, cuda), dev(yh, cuda)).cpu().numpy()
+    want, _, _ = o.iir(b, a, x, xh, yh)
+    e = err(y, want)
+    print(f"order={order} n={n} err={e:.2e}")
+    assert e <= IIR_TOL

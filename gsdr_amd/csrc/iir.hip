@@ -16,6 +16,9 @@
 //      state M^r S_group + prefix_(r-1) at once (table of M^r, r < 64, per level).
 //   3. k_iir_chunks<kFinal>: each chunk re-runs from its true start state and writes y.
 //   4. k_iir_history: the caller's history buffers receive the last P inputs / outputs.
+// For P <= 8 level 0's up-sweep runs inside the tails pass and its down-sweep in the final pass; up to
+// 2^25 samples the levels above 1 and level 1's down-sweep take one launch (k_iir_scan_upper), so 2^24
+// samples run as tails, level-1 up-sweep, upper scan, final: 4 launches.
 // State, scan and matrices are double (see Acc below); complex samples with real coefficients are
 // two independent recursions sharing M. State dimensions are padded to a compiled P (zero
 // coefficients beyond K-1 leave the recursion unchanged).

@@ -437,7 +437,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
 // the I column and R / S those of the Q column, y' = (P - S) + j (R + Q'): lane (q, n) and lane
 // (q ^ 2, n ^ 1) hold the two terms of one component, one lane exchange apart.
 // FM tiles overlap by 16 outputs (stride KT - 16, so every tile start stays a 16-multiple of the absolute
-// output index); the tile's y' go through LDS to the discriminator pass (coalesced 4-byte stores).
+// output index); each lane keeps its y' in registers and takes y'[k + 1] from the lane holding it (one
+// exchange per C tile; only a wave's last output reads the next wave's first through LDS).
 // Normwise parity with the float chains, not bit identity (gsdr_ext.h).
 // ------------------------------------------------------------------------------------------------
 template <int MODE, int NCT_ = 4>
@@ -461,7 +462,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
   using C = I8ChainMfma<MODE, NCT>;
   constexpr int D = C::D;
   __shared__ __attribute__((aligned(16))) char lds[C::LDS_BYTES];
-  __shared__ float2 ybuf[MODE == kModeFm ? C::KT : 1];  // FM: the tile's FIR outputs y'
+  __shared__ float2 wfirst[MODE == kModeFm ? C::WG / 64 : 1];  // FM: each wave's first y' of the tile
   __shared__ float wmax[C::WG / 64];
   __shared__ uint32_t wbad[C::WG / 64];
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
@@ -539,6 +540,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
   const uint32_t sg_acc = (is_re && hi) ? 0x80000000u : 0u, sg_oth = (is_re && !hi) ? 0x80000000u : 0u;
   const char* bplane = lds + (c ? C::PLANE : 0u);
   const uint32_t w = tid >> 6;
+  // FM: this lane's output within its C tile, o = 8 b + 4 (q & 1) + sel, and the lane holding o + 1
+  // (the inverse of the map: offset m = o' & 7 sits in lane quarter ((m >> 1) & 1) * 2 + (m >> 2), column
+  // parity (m ^ (m >> 1)) & 1); o = 63's neighbour is the next C tile's output 0 (lane 0)
+  const uint32_t o_lane = 8u * b + 4u * (q & 1u) + sel;
+  const uint32_t o_next = (o_lane + 1u) & 63u, m_next = o_next & 7u;
+  const int nb_lane = (int)(16u * (((m_next >> 1) & 1u) * 2u + (m_next >> 2)) + 2u * (o_next >> 3) +
+                            ((m_next ^ (m_next >> 1)) & 1u));
+  float2 ycur[MODE == kModeFm ? C::NCT : 1];
   I8Stage<4, C::SPAN, C::WG> st;
   if (blockIdx.x < tiles) i8_load_granules<4, LM>(st, p, ((int64_t)blockIdx.x * C::STRIDE - phase) * D + p.in_off);
   for (uint32_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
@@ -586,26 +595,44 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
       const uint32_t mi = __float_as_uint(mine), gi = __float_as_uint(got);
       const float2 y = make_float2(__uint_as_float((gi & b0mask) | (mi & ~b0mask)),
                                    __uint_as_float((mi & b0mask) | (gi & ~b0mask)));
-      const uint32_t rr = cbase + 8u * b + 4u * (q & 1u) + sel;  // this lane's output within the tile
+      const uint32_t rr = cbase + o_lane;  // this lane's output within the tile
       if constexpr (MODE == kModeAm) {
         const int64_t k = k_t + rr;
         if (k >= 0 && (uint64_t)k < p.N) out[k] = am_env(y);
       } else {
-        ybuf[rr] = y;
+        ycur[ct] = y;
+        if (ct == 0 && lane == 0u) wfirst[w] = y;  // output 0 of the wave's first C tile
       }
     }
     if constexpr (MODE == kModeFm) {
-      // one barrier for both the planes (read by every wave's MFMAs) and y' (read across waves below); the
-      // next tile's staging barrier orders this pass's reads before the next writes of ybuf
+      // One barrier for the planes (read by every wave's MFMAs) and the waves' first outputs; the next tile's
+      // staging barrier orders the reads of wfirst below before its next writes. Every other neighbour
+      // y'[k + 1] is in this wave's registers: one lane exchange per C tile.
       __syncthreads();
-      // two outputs a thread and step on packed FMAs (disc_angle2); r1 = r0 + WG
-      for (uint32_t r0 = tid; r0 < (uint32_t)C::STRIDE; r0 += 2u * C::WG) {
-        const uint32_t r1 = r0 + C::WG < (uint32_t)C::STRIDE ? r0 + C::WG : r0;
-        const float2 za = disc_product(ybuf[r0], ybuf[r0 + 1]), zb = disc_product(ybuf[r1], ybuf[r1 + 1]);
+      // (every exchange runs on all lanes: a lane exchange reads only active lanes' registers)
+      const float2 wnext = wfirst[w + 1u < C::WG / 64u ? w + 1u : w];
+      float2 ynx[C::NCT];
+#pragma unroll
+      for (int ct = 0; ct < C::NCT; ++ct) {
+        const float nx = __shfl(ycur[ct].x, nb_lane, 64), ny = __shfl(ycur[ct].y, nb_lane, 64);
+        // o = 63: the next C tile's output 0 (lane 0), or for the wave's last C tile the next wave's first
+        float2 first = wnext;
+        if (ct + 1 < C::NCT) {
+          const int cn = ct + 1 < C::NCT ? ct + 1 : ct;
+          first = make_float2(__shfl(ycur[cn].x, 0, 64), __shfl(ycur[cn].y, 0, 64));
+        }
+        ynx[ct] = o_lane == 63u ? first : make_float2(nx, ny);
+      }
+      // two outputs a lane and step on packed FMAs (disc_angle2): C tiles (0, 1), (2, 3), ...
+#pragma unroll
+      for (int ct = 0; ct < C::NCT; ct += 2) {
+        const int cb = ct + 1 < C::NCT ? ct + 1 : ct;
+        const float2 za = disc_product(ycur[ct], ynx[ct]), zb = disc_product(ycur[cb], ynx[cb]);
         const gsdr_f32x2 a2 = disc_angle2(za, zb) + gsdr_f32x2{dphi, dphi};
         float ang[2] = {a2.x, a2.y};
         const float2 zz[2] = {za, zb};
-        const uint32_t rr[2] = {r0, r1};
+        const float2 y0s[2] = {ycur[ct], ycur[cb]}, y1s[2] = {ynx[ct], ynx[cb]};
+        const uint32_t rr[2] = {(w * C::NCT + (uint32_t)ct) * 64u + o_lane, (w * C::NCT + (uint32_t)cb) * 64u + o_lane};
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           ang[h] = ang[h] > 3.14159274f ? ang[h] - 6.28318548f : (ang[h] <= -3.14159274f ? ang[h] + 6.28318548f : ang[h]);
@@ -614,7 +641,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
             // beside a nonzero one, silence, zero taps) gives the reference's atan2f(+-0, +-0) (fm.cu:66-68),
             // whose value (0 or +-pi) follows the signs of the ROTATED outputs y = e^{j phi(4k)} y': rotate
             // the nonzero ones; a zero window's y is +0 + j0 in the reference's ascending sum from +0
-            const float2 y0 = ybuf[rr[h]], y1 = ybuf[rr[h] + 1];
+            const float2 y0 = y0s[h], y1 = y1s[h];
             const uint32_t n = p.nco_n0 + 4u * (uint32_t)(k_t + rr[h]);
             const float2 u0 = (y0.x == 0.0f && y0.y == 0.0f) ? make_float2(0.0f, 0.0f)
                                                              : cmul(y0, nco_direct(n * p.nco_inc));
@@ -623,10 +650,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
             const float2 zr = disc_product(u0, u1);
             ang[h] = atan2f(zr.y, zr.x);
           }
+          const int64_t k = k_t + rr[h];
+          if ((h == 0 || cb != ct) && rr[h] < (uint32_t)C::STRIDE && k >= 0 && (uint64_t)k < p.N) {
+            out[k] = p.fm_gain * ang[h];
+          }
         }
-        const int64_t k0 = k_t + r0, k1 = k_t + r1;
-        if (k0 >= 0 && (uint64_t)k0 < p.N) out[k0] = p.fm_gain * ang[0];
-        if (r1 != r0 && k1 >= 0 && (uint64_t)k1 < p.N) out[k1] = p.fm_gain * ang[1];
       }
     } else {
       __syncthreads();  // every wave is done reading the tile's planes

@@ -308,23 +308,16 @@ hipError_t launch_multi_chain(const FirJob& j, const MultiParams& mp, hipStream_
 // int8 I/Q FIR on the matrix cores (k_fir_i8_mfma, fir_i8_mfma.hpp): D = 4, T <= 196; persistent
 // workgroups (their tap fragments are built once). The tile grid starts at output -out_phase, so the
 // staging granule and the output pairs are aligned per call from the pointers and the phase.
-template <int D, int NS, int BPC>
-hipError_t launch_i8_mfma_ns(const FirJob& j, hipStream_t s) {
-  using C = I8Mfma<D, NS>;
-  FirParams p = make_params(j);
-  const uint32_t ns = (uint32_t)ceil_div<uint64_t>(15u * D + j.T, 32u);
-  const uint64_t tiles = ceil_div<uint64_t>(j.N + p.out_phase, (uint64_t)C::KT);
-  if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
-  int cus = 0;
-  const hipError_t e = current_device_cus(&cus);
-  if (e != hipSuccess) return e;
-  const uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)cus * BPC);
+template <int D, int NS, int BPC, int NCT>
+hipError_t launch_i8_mfma_nct(const FirJob& j, const FirParams& p, uint32_t ns, uint64_t tiles, uint32_t grid,
+                              hipStream_t s) {
+  using C = I8Mfma<D, NS, NCT>;
   // tile starts are at sample (j KT - phase) D + in_off: byte offset 2 D (j KT - phase) + 2 in_off
   const uintptr_t in0 = reinterpret_cast<uintptr_t>(j.in) + (uintptr_t)(2 * j.in_off) - 2u * D * p.out_phase;
   const bool oa = ((reinterpret_cast<uintptr_t>(j.out) - 8u * p.out_phase) % 16) == 0;
-#define GSDR_I8_LAUNCH(G, LM)                                                                              \
-  (oa ? (k_fir_i8_mfma<D, NS, G, LM, true, BPC><<<dim3(grid), dim3(C::WG), 0, s>>>(p, ns, (uint32_t)tiles), 0) \
-      : (k_fir_i8_mfma<D, NS, G, LM, false, BPC><<<dim3(grid), dim3(C::WG), 0, s>>>(p, ns, (uint32_t)tiles), 0))
+#define GSDR_I8_LAUNCH(G, LM)                                                                                     \
+  (oa ? (k_fir_i8_mfma<D, NS, G, LM, true, BPC, NCT><<<dim3(grid), dim3(C::WG), 0, s>>>(p, ns, (uint32_t)tiles), 0) \
+      : (k_fir_i8_mfma<D, NS, G, LM, false, BPC, NCT><<<dim3(grid), dim3(C::WG), 0, s>>>(p, ns, (uint32_t)tiles), 0))
   if (in0 % 16 == 0) {
     (void)GSDR_I8_LAUNCH(8, 1);
   } else if (in0 % 8 == 0) {
@@ -336,6 +329,29 @@ hipError_t launch_i8_mfma_ns(const FirJob& j, hipStream_t s) {
   }
 #undef GSDR_I8_LAUNCH
   return launch_status();
+}
+
+template <int D, int NS, int BPC>
+hipError_t launch_i8_mfma_ns(const FirJob& j, hipStream_t s) {
+  FirParams p = make_params(j);
+  const uint32_t ns = (uint32_t)ceil_div<uint64_t>(15u * D + j.T, 32u);
+  int cus = 0;
+  const hipError_t e = current_device_cus(&cus);
+  if (e != hipSuccess) return e;
+  const uint64_t slots = (uint64_t)cus * BPC;
+  const uint64_t tiles = ceil_div<uint64_t>(j.N + p.out_phase, (uint64_t)I8Mfma<D, NS>::KT);
+  if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
+  if constexpr (BPC == 3) {
+    // A short call (fewer 2,048-output tiles than two rounds of workgroup slots) takes 512-output tiles:
+    // one large tile alone is ~10 us (load, 24 MFMAs a wave, stores), so a call of a few hundred tiles
+    // was one tile's latency on a third of the slots. Same outputs bit for bit (the summation order is
+    // per 16-output block, aligned to the absolute output index).
+    if (tiles < 2 * slots) {
+      const uint64_t t1 = ceil_div<uint64_t>(j.N + p.out_phase, (uint64_t)I8Mfma<D, NS, 1>::KT);
+      return launch_i8_mfma_nct<D, NS, BPC, 1>(j, p, ns, t1, (uint32_t)std::min<uint64_t>(t1, slots), s);
+    }
+  }
+  return launch_i8_mfma_nct<D, NS, BPC, 4>(j, p, ns, tiles, (uint32_t)std::min<uint64_t>(tiles, slots), s);
 }
 
 template <int D, int BPC = 3>
@@ -356,18 +372,10 @@ hipError_t launch_i8_mfma(const FirJob& j, hipStream_t s) {
 #ifndef GSDR_CHAIN_BPC
 #define GSDR_CHAIN_BPC 3
 #endif
-template <int MODE>
-hipError_t launch_chain_i8_mfma(const FirJob& j, hipStream_t s) {
-  constexpr int NCT = GSDR_CHAIN_NCT, BPC = GSDR_CHAIN_BPC;
+template <int MODE, int NCT, int BPC>
+hipError_t launch_chain_i8_mfma_nct(const FirJob& j, const FirParams& p, uint32_t ns, uint64_t tiles, uint32_t grid,
+                                    hipStream_t s) {
   using C = I8ChainMfma<MODE, NCT>;
-  FirParams p = make_params(j);
-  const uint32_t ns = (uint32_t)ceil_div<uint64_t>(7u * 4u + j.T, 32u);
-  const uint64_t tiles = ceil_div<uint64_t>(j.N + p.out_phase, (uint64_t)C::STRIDE);
-  if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
-  int cus = 0;
-  const hipError_t e = current_device_cus(&cus);
-  if (e != hipSuccess) return e;
-  const uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)cus * BPC);
   // tile starts are at sample 4 (j STRIDE - phase) + in_off: 8 (j STRIDE - phase) + 2 in_off bytes
   const uintptr_t in0 = reinterpret_cast<uintptr_t>(j.in) + (uintptr_t)(2 * j.in_off);
   if (in0 % 8 == 0) {
@@ -378,6 +386,27 @@ hipError_t launch_chain_i8_mfma(const FirJob& j, hipStream_t s) {
     k_chain_i8_mfma<MODE, 0, BPC, NCT><<<dim3(grid), dim3(C::WG), 0, s>>>(p, ns, (uint32_t)tiles);
   }
   return launch_status();
+}
+
+template <int MODE>
+hipError_t launch_chain_i8_mfma(const FirJob& j, hipStream_t s) {
+  constexpr int NCT = GSDR_CHAIN_NCT, BPC = GSDR_CHAIN_BPC;
+  FirParams p = make_params(j);
+  const uint32_t ns = (uint32_t)ceil_div<uint64_t>(7u * 4u + j.T, 32u);
+  const uint64_t tiles = ceil_div<uint64_t>(j.N + p.out_phase, (uint64_t)I8ChainMfma<MODE, NCT>::STRIDE);
+  if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
+  int cus = 0;
+  const hipError_t e = current_device_cus(&cus);
+  if (e != hipSuccess) return e;
+  const uint64_t slots = (uint64_t)cus * BPC;
+  if constexpr (NCT > 1) {
+    // short calls take one C tile a wave (as launch_i8_mfma_ns); the outputs are the same bit for bit
+    if (tiles < 2 * slots) {
+      const uint64_t t1 = ceil_div<uint64_t>(j.N + p.out_phase, (uint64_t)I8ChainMfma<MODE, 1>::STRIDE);
+      return launch_chain_i8_mfma_nct<MODE, 1, BPC>(j, p, ns, t1, (uint32_t)std::min<uint64_t>(t1, slots), s);
+    }
+  }
+  return launch_chain_i8_mfma_nct<MODE, NCT, BPC>(j, p, ns, tiles, (uint32_t)std::min<uint64_t>(tiles, slots), s);
 }
 
 // tile-shape sweep for the int8 front end (gsdrxFirFCInt8Variant): the shapes of launch_d4_complex

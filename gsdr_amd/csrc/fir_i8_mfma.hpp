@@ -296,10 +296,10 @@ __device__ __forceinline__ void i8_store_planes(const I8Stage<G, SPAN, WG>& st, 
   }
 }
 
-template <int D, int NS_>
+template <int D, int NS_, int NCT_ = 4>
 struct I8Mfma {
   static constexpr int WG = 256;
-  static constexpr int NCT = 4;                     // C tiles (128 outputs) per wave and tile
+  static constexpr int NCT = NCT_;                  // C tiles (128 outputs) per wave and tile
   static constexpr int KT = (WG / 64) * NCT * 128;  // outputs per tile (a multiple of 16)
   static constexpr int MAXNS = NS_;                 // 32-sample K steps: 15 D + T <= 32 NS
   static constexpr int MAXT = 32 * MAXNS - 15 * D;
@@ -313,9 +313,11 @@ struct I8Mfma {
 
 // BPC workgroups per CU (one wave per SIMD each): the register budget is 512 / BPC VGPRs.
 // G / LM: staging granule and load mode (I8Stage, i8_load_granules); OA: the output pairs (k, k + 1) are 16-byte aligned.
-template <int D, int NS, int G, int LM, bool OA, int BPC>
+// NCT: C tiles per wave and tile (4; 1 for short calls, whose few large tiles would leave most workgroup
+// slots idle -- an output's summation order does not depend on the tile size, only on its 16-output block)
+template <int D, int NS, int G, int LM, bool OA, int BPC, int NCT = 4>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC))) void k_fir_i8_mfma(FirParams p, uint32_t ns, uint32_t tiles) {
-  using C = I8Mfma<D, NS>;
+  using C = I8Mfma<D, NS, NCT>;
   __shared__ __attribute__((aligned(16))) char lds[C::LDS_BYTES];
   __shared__ float wmax[C::WG / 64];
   __shared__ uint32_t wbad[C::WG / 64];

@@ -557,3 +557,38 @@ def test_int8_stream_one_launch(cuda, kind, case):
     torch.cuda.synchronize()
     assert got.numel() == want.numel()
     assert got.cpu().numpy().tobytes() == want.cpu().numpy().tobytes()
+
+
+def test_fir_int8_mfma_tile_shapes_bit_identical(cuda):
+    """Calls with fewer large tiles than two rounds of workgroup slots take 512-output tiles instead of
+    2,048-output ones (fir_dispatch.hpp launch_i8_mfma_ns). The summation order is per 16-output block,
+    aligned to the absolute output index, so the shapes agree bit for bit: config 2's int8 channel in one
+    call (large tiles) against the same channel through the streaming object in 64 chunks (small tiles),
+    and against the oracle's normwise bar."""
+    from gsdr_amd import ops
+    from gsdr_amd.signals import lowpass_taps
+    from gsdr_amd.stream import Stream
+
+    D, T = 4, 127
+    L = 67_108_987
+    N = (L - T) // D + 1
+    g = torch.Generator(device=cuda).manual_seed(64)
+    xd = torch.randint(-128, 128, (2 * L,), dtype=torch.int8, device=cuda, generator=g)
+    td = dev(lowpass_taps(T, 0.1), cuda)
+    whole = ops.fir(td, xd, D, N)
+    s = Stream("fir", td, D, 1.0, 0.0, 0.0, 1.0, first_sample_index=0, int8=True)
+    cs = L // 64 + 1  # odd: chunk starts alternate between 2-byte and 4-byte alignment
+    parts, pos = [], 0
+    while pos < L:
+        m = min(cs, L - pos)
+        parts.append(s.process(xd[2 * pos:2 * (pos + m)]).clone())
+        pos += m
+    s.close()
+    got = torch.cat(parts)[:N]
+    assert torch.equal(got.view(torch.float32), whole.view(torch.float32))
+    # a window of the whole call against the oracle (the bar the header states)
+    k0, n = 12_345_677, 4096
+    raw = xd[2 * k0 * D:2 * ((k0 + n - 1) * D + T)].cpu().numpy()
+    xf = as_complex(o.int8_to_float(raw))
+    taps = lowpass_taps(T, 0.1)
+    assert normwise_err(host(whole[k0:k0 + n]), o.fir(taps, xf, D, n), bound(taps, xf, D, n)) <= FLOAT_TOL

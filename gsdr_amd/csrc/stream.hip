@@ -101,8 +101,46 @@ hipError_t filter(const gsdrxStream_t& s, const void* in, uint64_t first, void* 
   }
 }
 
-hipError_t copy(void* dst, const void* src, size_t bytes, hipStream_t st) {
-  return bytes ? hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st) : hipSuccess;
+// The small device-to-device moves of one call (seam = history + chunk head, next history = the tail of
+// old history + chunk), gathered into ONE launch: as separate hipMemcpyAsync calls each was a runtime blit
+// launch of ~4-5 us, four of them per call, which is what a short float call paid (tools/float_stream_time.py).
+// Segments never overlap (they write seam / spare and read hist / the chunk).
+struct Gather {
+  static constexpr int kMax = 4;
+  struct Seg {
+    char* dst;
+    const char* src;
+    uint64_t bytes;
+  } seg[kMax];
+  int n = 0;
+  void add(void* dst, const void* src, size_t bytes) {
+    if (bytes) seg[n++] = Seg{static_cast<char*>(dst), static_cast<const char*>(src), bytes};
+  }
+};
+
+__global__ __launch_bounds__(256) void k_stream_gather(Gather g) {
+  for (int i = 0; i < g.n; ++i) {
+    const Gather::Seg sg = g.seg[i];
+    // 4-byte moves when both ends and the length allow (every sample format is 2 or 8 bytes)
+    if (((reinterpret_cast<uintptr_t>(sg.dst) | reinterpret_cast<uintptr_t>(sg.src) | sg.bytes) & 3u) == 0) {
+      uint32_t* d = reinterpret_cast<uint32_t*>(sg.dst);
+      const uint32_t* s = reinterpret_cast<const uint32_t*>(sg.src);
+      for (uint64_t k = threadIdx.x + (uint64_t)blockIdx.x * blockDim.x; k < sg.bytes / 4; k += (uint64_t)gridDim.x * blockDim.x)
+        d[k] = s[k];
+    } else {
+      for (uint64_t k = threadIdx.x + (uint64_t)blockIdx.x * blockDim.x; k < sg.bytes; k += (uint64_t)gridDim.x * blockDim.x)
+        sg.dst[k] = sg.src[k];
+    }
+  }
+}
+
+hipError_t gather(const Gather& g, hipStream_t st) {
+  if (g.n == 0) return hipSuccess;
+  uint64_t most = 0;
+  for (int i = 0; i < g.n; ++i) most = std::max<uint64_t>(most, g.seg[i].bytes);
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>(64, ceil_div<uint64_t>(most, 256u * 4u));
+  k_stream_gather<<<blocks, 256, 0, st>>>(g);
+  return launch_status();
 }
 
 }  // namespace
@@ -215,26 +253,29 @@ GSDR_C_LINKAGE hipError_t gsdrxStreamProcess(gsdrxStream s, const void* input, s
     if (e != hipErrorNotSupported) return e;
     e = hipSuccess;  // not this shape: the seam path below
   }
+  // every small move of the call (seam assembly, next history) in one launch ahead of the filters
+  gsdr::Gather g;
   if (p.n_seam) {
-    e = gsdr::copy(s->seam, s->hist, h * s->sb, cudaStream);
-    if (e == hipSuccess) e = gsdr::copy(s->seam + h * s->sb, chunk, p.head * s->sb, cudaStream);
-    if (e == hipSuccess) e = gsdr::filter(*s, s->seam, s->n0 + h0, out, p.n_seam, cudaStream);
+    g.add(s->seam, s->hist, h * s->sb);
+    g.add(s->seam + h * s->sb, chunk, p.head * s->sb);
   }
-  if (e == hipSuccess && p.n_main) {
-    e = gsdr::filter(*s, chunk + p.main_off * s->sb, s->n0 + p.m_mid * s->D, out + p.n_seam * s->ob, p.n_main,
-                     cudaStream);
-  }
-  if (e == hipSuccess && p.hist_after) {
+  if (p.hist_after) {
     const uint64_t from = p.m_end * s->D, S_new = S + numInputSamples;
     uint64_t done = 0;
     if (from < S) {  // part of the new history is still in the old one
       done = S - from;
-      e = gsdr::copy(s->spare, s->hist + (from - h0) * s->sb, done * s->sb, cudaStream);
+      g.add(s->spare, s->hist + (from - h0) * s->sb, done * s->sb);
     }
     const uint64_t c0 = from > S ? from - S : 0;
-    if (e == hipSuccess) e = gsdr::copy(s->spare + done * s->sb, chunk + c0 * s->sb, (S_new - S - c0) * s->sb, cudaStream);
-    std::swap(s->hist, s->spare);
+    g.add(s->spare + done * s->sb, chunk + c0 * s->sb, (S_new - S - c0) * s->sb);
   }
+  e = gsdr::gather(g, cudaStream);
+  if (e == hipSuccess && p.n_seam) e = gsdr::filter(*s, s->seam, s->n0 + h0, out, p.n_seam, cudaStream);
+  if (e == hipSuccess && p.n_main) {
+    e = gsdr::filter(*s, chunk + p.main_off * s->sb, s->n0 + p.m_mid * s->D, out + p.n_seam * s->ob, p.n_main,
+                     cudaStream);
+  }
+  if (e == hipSuccess && p.hist_after) std::swap(s->hist, s->spare);
   if (e != hipSuccess) return e;
   s->consumed += numInputSamples;
   s->next_out = p.m_end;

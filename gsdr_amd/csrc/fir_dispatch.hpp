@@ -433,6 +433,22 @@ inline hipError_t launch_d4_int8(const FirJob& j, hipStream_t s) {
       return launch_i8_mfma<4, 4>(j, s);
     case 41:  // matrix cores, 3 workgroups per CU: the default for D = 4
       return launch_i8_mfma<4, 3>(j, s);
+    case 42:  // matrix cores, 3 workgroups per CU, 1,024-output tiles at every size (tile-shape sweep)
+    case 43: {  // the same with 512-output tiles
+      if (j.D != 4 || j.T < 1 || j.T > (size_t)I8Mfma<4, 6>::MAXT || (reinterpret_cast<uintptr_t>(j.out) % 8) != 0) {
+        return hipErrorInvalidValue;
+      }
+      const FirParams p = make_params(j);
+      const uint32_t ns = (uint32_t)ceil_div<uint64_t>(15u * 4u + j.T, 32u);
+      int cus = 0;
+      const hipError_t e = current_device_cus(&cus);
+      if (e != hipSuccess) return e;
+      const uint64_t kt = j.variant == 42 ? (uint64_t)I8Mfma<4, 6, 2>::KT : (uint64_t)I8Mfma<4, 6, 1>::KT;
+      const uint64_t t = ceil_div<uint64_t>(j.N + p.out_phase, kt);
+      const uint32_t grid = (uint32_t)std::min<uint64_t>(t, (uint64_t)cus * 3);
+      return j.variant == 42 ? launch_i8_mfma_nct<4, 6, 3, 2>(j, p, ns, t, grid, s)
+                             : launch_i8_mfma_nct<4, 6, 3, 1>(j, p, ns, t, grid, s);
+    }
     default:
       return hipErrorInvalidValue;
   }

@@ -33,7 +33,7 @@ $(BUILD)/probes/fir.o: gsdr_amd/csrc/fir.hip $(HDRS)
 $(BUILD)/probes/libgsdr_probes.so: $(filter-out $(BUILD)/fir.o,$(OBJS)) $(BUILD)/probes/fir.o
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -Wl,-rpath,/opt/rocm/lib $^ -o $@
 
-oracle/build/liboracle.so: oracle/gsdr_oracle.c oracle/gsdr_oracle.h gsdr_amd/csrc/awgn_table.inc
+oracle/build/liboracle.so: oracle/gsdr_oracle.c oracle/gsdr_oracle.h gsdr_amd/csrc/awgn_table.inc gsdr_amd/csrc/awgn_tail_table.inc
 	@mkdir -p oracle/build
 	$(CC) $(OFLAGS) -shared oracle/gsdr_oracle.c -o $@ -lm -lpthread
 

@@ -14,7 +14,14 @@
 //     (float)(2a + 1) (exact) gives index = (bits >> 18) - 127 * 32 (its exponent and top 5 mantissa bits)
 //     and f = (bits & 0x3ffff) 2^-18 (exact), |g| = fmaf(S, f, R) -- within 2.5e-5 of h, unbiased (the
 //     table holds S 2^-18, so the product is S' times the integer: the same bits, one multiply fewer).
-//     Tails are cut at h(2^-21) = 5.035 sigma.
+//   * Tail extension (round 4): a component whose a < 32 (v < 2^-15, |g| > 4.17) takes 18 more bits e
+//     from a second Philox block of the same key (counter (k / 3 lo, hi, 1, 0)): component c of the
+//     block (slot s: c = 2s for the first normal, 2s + 1 for the second) uses x0 >> 14, x1 >> 14,
+//     x2 >> 14, x3 >> 14, (x0 & 0x3fff) << 4 | (x2 & 0xf), (x1 & 0x3fff) << 4 | (x3 & 0xf) for c = 0..5.
+//     Then x' = 2 (a 2^18 + e) + 1 < 2^24 (exact in float), v' = x' 2^-39, and |g| is read the same way
+//     from a 24 x 32 tail table (awgn_tail_table.inc): the tails reach h(2^-39) = 7.0 sigma, where a
+//     single 21-bit draw cut them at h(2^-21) = 5.035 (P(|g| > 5.035) = 4.8e-7 per axis had been lost).
+//     ~3e-5 of the components take it; the second Philox block is evaluated only then.
 // Every operation is exact or one correctly rounded IEEE fmaf, so the host restatement
 // (oracle/gsdr_oracle.c, which reads the same table) reproduces every bit. Round 2's Box-Muller with
 // correctly rounded sqrt and polynomial ln / sin / cos cost ~320 of the ~450 cycles per symbol and wave.
@@ -34,6 +41,15 @@ __constant__ float2 c_awgn_table[kAwgnTableSize] = {
 #undef GSDR_AWGN_ENTRY
 };
 
+constexpr int kAwgnTailSize = 24 * 32;
+
+// (R, S) pairs of the tail extension: read straight from this array (rarely: ~3e-5 of the components).
+__constant__ float2 c_awgn_tail[kAwgnTailSize] = {
+#define GSDR_AWGN_ENTRY(r, s) {r, s},
+#include "awgn_tail_table.inc"
+#undef GSDR_AWGN_ENTRY
+};
+
 // a ^ b ^ k in one v_bitop3_b32 (gfx950; the compiler emits two v_xor_b32), k wave-uniform (the key)
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t k) {
   uint32_t r;
@@ -41,12 +57,18 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t k) {
   return r;
 }
 
-__device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
-                                              uint32_t k1, uint32_t (&w)[4]) {
-#pragma unroll
+// GSDR_PHILOX_ROUNDS: a timing probe (tools/awgn_time.py builds): any other round count changes every
+// noise sample, so it is refused outside the probe builds (-DGSDR_TUNING_PROBES).
 #ifndef GSDR_PHILOX_ROUNDS
 #define GSDR_PHILOX_ROUNDS 10
 #endif
+#if GSDR_PHILOX_ROUNDS != 10 && !defined(GSDR_TUNING_PROBES)
+#error "GSDR_PHILOX_ROUNDS != 10 breaks the channel's bit parity with the oracle: probe builds only"
+#endif
+
+__device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
+                                              uint32_t k1, uint32_t (&w)[4]) {
+#pragma unroll
   for (int r = 0; r < GSDR_PHILOX_ROUNDS; ++r) {
     // one 32 x 32 -> 64-bit product per multiplier (v_mad_u64_u32) instead of separate mul_lo / mul_hi:
     // both are quarter-rate, and these 40 products per three symbols bound the kernel
@@ -79,17 +101,61 @@ __device__ __forceinline__ float awgn_normal(const float2* __restrict__ tab, uin
   return __uint_as_float(__float_as_uint(m) ^ ((r << 11) & 0x80000000u));
 }
 
+// The tail normal of a component with a = r & 0xfffff < 32 and its 18 extension bits e.
+__device__ __forceinline__ float awgn_tail_normal(uint32_t r, uint32_t e) {
+  const uint32_t x = ((((r & 0x1fu) << 18) | e) << 1) | 1u;  // < 2^24: exact in float
+  const uint32_t b = __float_as_uint((float)x);
+  const float2 rs = c_awgn_tail[(b >> 18) - 127u * 32u];
+  const float m = fmaf(rs.y, (float)(b & 0x3ffffu), rs.x);
+  return __uint_as_float(__float_as_uint(m) ^ ((r << 11) & 0x80000000u));
+}
+
+__device__ __forceinline__ bool awgn_in_tail(uint32_t r) { return (r & 0xfffe0u) == 0u; }
+
 // The Philox block holding absolute symbols 3 blk .. 3 blk + 2.
 __device__ __forceinline__ void awgn_block_words(uint64_t seed, uint64_t blk, uint32_t (&w)[4]) {
   philox4x32_10((uint32_t)blk, (uint32_t)(blk >> 32), 0u, 0u, (uint32_t)seed, (uint32_t)(seed >> 32), w);
 }
 
-// The normal pair of slot `slot` (0..2, compile-time after unrolling) of a block.
-__device__ __forceinline__ float2 awgn_slot(const float2* __restrict__ tab, const uint32_t (&w)[4], int slot) {
-  if (slot == 0) return make_float2(awgn_normal(tab, w[0] >> 11), awgn_normal(tab, w[1] >> 11));
-  if (slot == 1) return make_float2(awgn_normal(tab, w[2] >> 11), awgn_normal(tab, w[3] >> 11));
-  return make_float2(awgn_normal(tab, ((w[0] & 0x7ffu) << 10) | ((w[1] & 0x7ffu) >> 1)),
-                     awgn_normal(tab, ((w[2] & 0x7ffu) << 10) | ((w[3] & 0x7ffu) >> 1)));
+// Both normals of slot `slot` when at least one of them is in the tail: the extension block, then the
+// tail-table value for each tail component (out of line: ~2e-4 of the lanes' blocks take it).
+__device__ __noinline__ float2 awgn_slot_tail(uint64_t seed, uint64_t blk, int slot, uint32_t r0, uint32_t r1,
+                                             float2 g) {
+  uint32_t x[4];
+  philox4x32_10((uint32_t)blk, (uint32_t)(blk >> 32), 1u, 0u, (uint32_t)seed, (uint32_t)(seed >> 32), x);
+  uint32_t e0, e1;
+  if (slot == 0) {
+    e0 = x[0] >> 14;
+    e1 = x[1] >> 14;
+  } else if (slot == 1) {
+    e0 = x[2] >> 14;
+    e1 = x[3] >> 14;
+  } else {
+    e0 = ((x[0] & 0x3fffu) << 4) | (x[2] & 0xfu);
+    e1 = ((x[1] & 0x3fffu) << 4) | (x[3] & 0xfu);
+  }
+  if (awgn_in_tail(r0)) g.x = awgn_tail_normal(r0, e0);
+  if (awgn_in_tail(r1)) g.y = awgn_tail_normal(r1, e1);
+  return g;
+}
+
+// The normal pair of slot `slot` (0..2, compile-time after unrolling) of block `blk` (words w).
+__device__ __forceinline__ float2 awgn_slot(const float2* __restrict__ tab, const uint32_t (&w)[4], int slot,
+                                            uint64_t seed, uint64_t blk) {
+  uint32_t r0, r1;
+  if (slot == 0) {
+    r0 = w[0] >> 11;
+    r1 = w[1] >> 11;
+  } else if (slot == 1) {
+    r0 = w[2] >> 11;
+    r1 = w[3] >> 11;
+  } else {
+    r0 = ((w[0] & 0x7ffu) << 10) | ((w[1] & 0x7ffu) >> 1);
+    r1 = ((w[2] & 0x7ffu) << 10) | ((w[3] & 0x7ffu) >> 1);
+  }
+  const float2 g = make_float2(awgn_normal(tab, r0), awgn_normal(tab, r1));
+  if (__builtin_expect(awgn_in_tail(r0) || awgn_in_tail(r1), 0)) return awgn_slot_tail(seed, blk, slot, r0, r1, g);
+  return g;
 }
 
 }  // namespace gsdr

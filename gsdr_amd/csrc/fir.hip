@@ -116,6 +116,43 @@ hipError_t launch_fc_probe(const FirJob& j, hipStream_t s) {
         default: return launch_poly<float, float2, 4, 4, 16, 256, kModeFm, 0, true, true>(c, s);
       }
     }
+    // LDS-read probe: the default kernel with the register window served from the
+    // thread's own R rows only (4 of 19 ds_read_b128 per column and chunk; wrong results, same FMAs):
+    // 140 full kernel, 141 compute only
+    case 140:
+      return launch_poly<float, float2, 4, 4, 16, 256, kModeFir, 64, true>(j, s);
+    case 141:
+      return launch_poly<float, float2, 4, 4, 16, 256, kModeFir, 66, true>(j, s);
+    // FM chain: 127 tile-relative NCO phasors by recurrence (one cmul a granule instead of the
+    // transcendental pair)
+    case 127: {
+      FirJob c = j;
+      c.mode = kModeFm;
+      c.N = j.N - 1;
+      c.nco_inc = 429496730u;
+      c.fm_gain = 7.957747f;
+      return launch_poly<float, float2, 4, 4, 16, 256, kModeFm, 128, true>(c, s);
+    }
+    // 128: persistent workgroups with tile-relative NCO phasors held in registers (k_fir_poly_rel)
+    case 128: {
+      FirJob c = j;
+      c.mode = kModeFm;
+      c.N = j.N - 1;
+      c.nco_inc = 429496730u;
+      c.fm_gain = 7.957747f;
+      using Geo = TileGeo<float2, 4, 4, 256>;
+      FirParams p = make_params(c);
+      p.nch = 2;
+      p.tile_stride = Geo::KT - 1;
+      const uint32_t tiles = (uint32_t)ceil_div<uint64_t>(c.N, p.tile_stride);
+      int cus = 0;
+      const hipError_t e = current_device_cus(&cus);
+      if (e != hipSuccess) return e;
+      const uint32_t grid = std::min<uint32_t>(tiles, (uint32_t)cus * 4u);
+      const size_t lds = poly_lds_bytes<float2, 4, 4, 256>(128, kModeFm);
+      k_fir_poly_rel<float, float2, 4, 4, 16, 256, kModeFm><<<dim3(grid), dim3(256), lds, s>>>(p, tiles);
+      return launch_status();
+    }
     case 110:
     case 111:
       return launch_stream_probe(j, s, j.variant == 111);
@@ -126,6 +163,31 @@ hipError_t launch_fc_probe(const FirJob& j, hipStream_t s) {
 #else
 hipError_t launch_fc_probe(const FirJob&, hipStream_t) { return hipErrorInvalidValue; }
 #endif  // GSDR_TUNING_PROBES
+
+// The streaming object's one-launch FIR step on complex float samples (stream.hip; stream_step_tiled).
+hipError_t fir_fc_stream_step(size_t decimation, const float* taps, size_t tapCount, const hipFloatComplex* chunk,
+                              uint64_t chunkLen, int64_t inOff, const hipFloatComplex* hist, uint64_t histLen,
+                              hipFloatComplex* histOut, int64_t histFrom, uint64_t histN, hipFloatComplex* output,
+                              size_t numOutputs, int32_t device, hipStream_t stream) {
+  FirJob job;
+  job.in = chunk;
+  job.taps = taps;
+  job.out = output;
+  job.D = decimation;
+  job.T = tapCount;
+  job.N = numOutputs;
+  job.L = chunkLen;
+  job.mode = kModeFir;
+  job.in_off = inOff;
+  job.hist = hist;
+  job.hist_len = histLen;
+  job.hist_out = histOut;
+  job.hist_from = histFrom;
+  job.hist_n = histN;
+  DeviceScope scope(device);
+  if (scope.status() != hipSuccess) return scope.status();
+  return stream_step_tiled<float2, kModeFir>(job, stream);
+}
 
 }  // namespace gsdr
 

@@ -45,6 +45,9 @@ struct FirJob {
   void* hist_out = nullptr;
   int64_t hist_from = 0;
   uint64_t hist_n = 0;
+  // the streaming object's one-launch path on the tiled kernels (stream_step_tiled): only the polyphase and
+  // contiguous-window kernels take it; the others return hipErrorNotSupported before launching anything
+  bool stream_tiled = false;
 };
 
 // LDS budget per workgroup for the tiled kernels (keeps >= 2 workgroups per CU on 160 KiB).
@@ -115,6 +118,7 @@ inline void launch_shifted(const void* in, F&& f) {
 
 template <class TapT, class InT, int MODE>
 hipError_t launch_generic(const FirJob& j, hipStream_t s) {
+  if (j.stream_tiled) return hipErrorNotSupported;
   FirParams p = make_params(j);
   const uint64_t blocks = ceil_div<uint64_t>(j.N, 256);
   if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
@@ -501,6 +505,7 @@ hipError_t launch_rt_wg(const FirJob& j, uint32_t nch, size_t lds, hipStream_t s
 template <class TapT, class InT, int MODE>
 hipError_t launch_rt(const FirJob& j, hipStream_t s) {
   constexpr int IC = 16;
+  if (j.stream_tiled) return hipErrorNotSupported;
   if (j.T <= j.D || j.D > 4096) return launch_generic<TapT, InT, MODE>(j, s);
   const uint32_t nch = (uint32_t)ceil_div<uint64_t>(j.T, (uint64_t)IC);
   const uint32_t D = (uint32_t)j.D, span = nch * IC;
@@ -591,14 +596,15 @@ hipError_t launch_fir(const FirJob& j, hipStream_t s) {
     // D = 4 FM / AM chains: the matrix-core kernel with the NCO folded into complex taps (normwise
     // parity with the float chains: DESIGN.md section 3.3); variant 0 keeps the exact path (streams)
     if constexpr (MODE != kModeFir && std::is_same<TapT, float>::value) {
-      if (j.D == 4 && j.variant < 0 && j.T <= (size_t)I8ChainMfma<MODE>::MAXT) {
+      if (j.D == 4 && j.variant < 0 && !j.stream_tiled && j.T <= (size_t)I8ChainMfma<MODE>::MAXT) {
         return launch_chain_i8_mfma<MODE>(j, s);
       }
     }
     // D = 4 FIR: the matrix-core kernel (bf16-exact samples, exact three-part taps; normwise parity with
     // the float path, twice its speed: DESIGN.md section 3.3)
     if constexpr (MODE == kModeFir && std::is_same<TapT, float>::value) {
-      if (j.D == 4 && j.T <= (size_t)I8Mfma<4, 8>::MAXT && (reinterpret_cast<uintptr_t>(j.out) % 8) == 0) {
+      if (j.D == 4 && !j.stream_tiled && j.T <= (size_t)I8Mfma<4, 8>::MAXT &&
+          (reinterpret_cast<uintptr_t>(j.out) % 8) == 0) {
         return launch_i8_mfma<4, 3>(j, s);
       }
     }
@@ -652,6 +658,22 @@ hipError_t launch_fir(const FirJob& j, hipStream_t s) {
         return launch_other_d<TapT, InT, MODE>(j, s);
     }
   }
+}
+
+// The streaming object's one-launch step on the tiled kernels (stream.hip): outputs [0, N) of the call,
+// output 0's window at chunk offset j.in_off (negative: it starts in the history j.hist of j.hist_len
+// samples), the next history (chunk offsets [hist_from, + hist_n)) copied by workgroup 0 of the same
+// launch. j.in is the chunk and j.L its length here. The kernels are the monolithic call's, tile for tile,
+// so the outputs are bit-identical to it. hipErrorNotSupported (nothing launched) when the shape runs
+// another kernel; the stream then takes its seam path.
+template <class InT, int MODE>
+hipError_t stream_step_tiled(FirJob j, hipStream_t s) {
+  if (j.N == 0 || j.T == 0 || j.taps == nullptr || j.T > (1u << 26)) return hipErrorNotSupported;
+  j.stream_tiled = true;
+  j.variant = -1;
+  j.in = static_cast<const InT*>(j.in) + j.in_off;  // output 0's window (may precede the chunk)
+  j.L = (uint64_t)((int64_t)j.L - j.in_off);         // samples readable from there
+  return launch_fir<float, InT, MODE>(j, s);
 }
 
 }  // namespace gsdr

@@ -191,10 +191,13 @@ struct FirParams {
   uint32_t nco_n0;       // low 32 bits of firstSampleIndex
   float fm_gain;         // FM discriminator gain
   uint32_t out_phase;    // absolute index of output 0 mod 16 (the int8 matrix-core kernels' block grid)
-  // int8 matrix-core kernels only (fir_i8_mfma.hpp; the streaming object's one-launch path): output 0's
-  // window starts at sample in_off of `in`; samples at negative offsets i >= -hist_len come from
-  // hist[hist_len + i] (the stream's history), and samples [hist_from, hist_from + hist_n) (same
-  // offsets) are copied to hist_out (the next history)
+  // The streaming object's one-launch path (stream.hip): output 0's window starts at sample in_off of the
+  // caller's chunk; chunk samples at negative offsets i >= -hist_len come from hist[hist_len + i] (the
+  // stream's history), and samples [hist_from, hist_from + hist_n) (same offsets) are copied to hist_out
+  // (the next history) by workgroup 0. The int8 matrix-core kernels (fir_i8_mfma.hpp) take `in` = the
+  // chunk and L = its length; the tiled kernels below take `in` = chunk + in_off (output 0's window, so
+  // the tile arithmetic is unchanged; the pointer may precede the chunk, and samples before it are read
+  // only through the history) and L = samples readable from there.
   int64_t in_off;
   const void* hist;
   uint64_t hist_len;
@@ -392,6 +395,55 @@ __device__ __forceinline__ bool stage_body_dma(float4* __restrict__ lds, const I
   }
 }
 
+// Streaming one-launch path (FirParams::hist != nullptr): local sample s of the tiled kernels (counted
+// from output 0's window start, `in` = chunk + in_off) is chunk sample s + in_off; the ones before the
+// chunk come from the history. Samples at or past L read as zero.
+template <class InT>
+__device__ __forceinline__ typename LdsSample<InT>::type stream_sample(const InT* __restrict__ in,
+                                                                        const FirParams& p, uint64_t s) {
+  using LdsT = typename LdsSample<InT>::type;
+  if (s >= p.L) {
+    LdsT z;
+    set_zero(z);
+    return z;
+  }
+  const int64_t i = (int64_t)s + p.in_off;
+  return i < 0 ? to_lds_sample(reinterpret_cast<const InT*>(p.hist)[(int64_t)p.hist_len + i]) : to_lds_sample(in[s]);
+}
+
+// A tile that reaches into the stream's history (only the first tile of a call: the history is shorter
+// than one window): one granule at a time through stream_sample.
+template <class InT, class Geo, int WG, int MODE>
+__device__ __forceinline__ void stage_tile_stream(float4* __restrict__ lds, const InT* __restrict__ in, uint64_t S0,
+                                                  uint32_t NG, const FirParams& p) {
+  constexpr int G = Geo::G;
+  for (uint32_t g = threadIdx.x; g < NG; g += WG) {
+    const uint64_t s = S0 + (uint64_t)g * G;
+    float4 v;
+    if constexpr (G == 2) {
+      const float2 a = stream_sample<InT>(in, p, s), b = stream_sample<InT>(in, p, s + 1);
+      v = make_float4(a.x, a.y, b.x, b.y);
+    } else {
+      v = make_float4(stream_sample<InT>(in, p, s), stream_sample<InT>(in, p, s + 1), stream_sample<InT>(in, p, s + 2),
+                      stream_sample<InT>(in, p, s + 3));
+    }
+    lds[Geo::padded(g)] = stage_transform<InT, MODE>(v, (uint32_t)s, p);
+  }
+}
+
+// The next history of a streaming call, copied by workgroup 0 (any time during the launch: it writes
+// the stream's spare buffer, which no tile reads).
+template <class InT>
+__device__ __forceinline__ void stream_copy_history(const FirParams& p) {
+  if (p.hist_out == nullptr || blockIdx.x != 0) return;
+  const InT* __restrict__ in = reinterpret_cast<const InT*>(p.in);  // chunk + in_off
+  InT* __restrict__ dst = reinterpret_cast<InT*>(p.hist_out);
+  for (uint64_t j = threadIdx.x; j < p.hist_n; j += blockDim.x) {
+    const int64_t i = p.hist_from + (int64_t)j;  // chunk offset
+    dst[j] = i < 0 ? reinterpret_cast<const InT*>(p.hist)[(int64_t)p.hist_len + i] : in[i - p.in_off];
+  }
+}
+
 // SH (complex or int8 I/Q samples): the input is one sample off its aligned granule load (complex: 8 bytes
 // off 16; int8 I/Q: 2 bytes off 4) at every tile start. The tile
 // body is then loaded as aligned 16-byte granules starting one sample early, and each loaded pair is
@@ -399,10 +451,14 @@ __device__ __forceinline__ bool stage_body_dma(float4* __restrict__ lds, const I
 // body's last slot whole. The NCO phasor is a function of the absolute index, so the odd-start pairs
 // mix exactly as the even-start ones would.
 template <class InT, class Geo, int WG, bool VEC, int MODE, bool NT = false, bool DMA = false, int SH = 0,
-          bool NODIRECT = false>
+          bool NODIRECT = false, bool REL = false>
 __device__ __forceinline__ void stage_tile(float4* __restrict__ lds, const InT* __restrict__ in, uint64_t S0,
                                            uint32_t NG, const FirParams& p) {
   constexpr int G = Geo::G;
+  if (p.hist != nullptr && (int64_t)S0 + p.in_off < 0) {  // uniform: the tile starts in the stream's history
+    stage_tile_stream<InT, Geo, WG, MODE>(lds, in, S0, NG, p);
+    return;
+  }
   // tile body granules per staging thread (Geo::KT / R output segments of SG granules over WG threads)
   constexpr int BPT = Geo::SG * (Geo::KT / Geo::ROUT) / WG;
   static_assert(BPT * WG == Geo::SG * (Geo::KT / Geo::ROUT), "tile body must split evenly over the threads");
@@ -419,7 +475,9 @@ __device__ __forceinline__ void stage_tile(float4* __restrict__ lds, const InT* 
     // granule g, written as two partial-granule LDS stores (8-byte aligned pieces). The halo re-writes
     // the body's last granule whole, as for complex input.
     static_assert(!VEC && SH > 0 && SH < 4, "shifted real staging: 1..3 floats off 16-byte alignment");
-    if (S0 + (uint64_t)NG * G <= p.L) {
+    // (a tile at S0 < SH would load SH floats before the caller's buffer -- inside in[0]'s 16-byte block, so
+    // it cannot fault, but it is out of bounds: that tile takes the per-granule loads below instead)
+    if (S0 >= (uint64_t)SH && S0 + (uint64_t)NG * G <= p.L) {
       float* __restrict__ l1 = reinterpret_cast<float*>(lds);
       const float4* __restrict__ src = reinterpret_cast<const float4*>(in + S0 - SH);  // 16-byte aligned
 #pragma unroll
@@ -457,7 +515,7 @@ __device__ __forceinline__ void stage_tile(float4* __restrict__ lds, const InT* 
   } else if constexpr (SH != 0) {
     static_assert((std::is_same<InT, float2>::value || std::is_same<InT, Iq8>::value) && !VEC && SH == 1,
                   "shifted staging is for 8-byte-aligned complex or 2-byte-aligned int8 I/Q input");
-    if (S0 + (uint64_t)NG * G <= p.L) {
+    if (S0 >= 1u && S0 + (uint64_t)NG * G <= p.L) {  // (S0 = 0 would load the sample before the buffer)
       float2* __restrict__ l2 = reinterpret_cast<float2*>(lds);
 #pragma unroll
       for (int b0 = 0; b0 < BPT; b0 += SB) {
@@ -512,6 +570,42 @@ __device__ __forceinline__ void stage_tile(float4* __restrict__ lds, const InT* 
   // The body loop, instantiated once per NCO start parity (`odd` is uniform over the tile): with the
   // parity a runtime value the compiler kept a branch around every granule's phasor.
   const uint32_t pbase = Geo::padded(tid);
+  if constexpr (REL && MODE != kModeFir) {
+    // tuning probe: tile-relative phasors by recurrence (granule k * WG + tid starts at tile-relative
+    // sample G (k WG + tid): its phasor is the previous granule's times F = phasor(G WG))
+    static_assert(G == 2, "complex samples");
+    const float2 w = nco_direct(p.nco_inc), F = nco_direct((uint32_t)(WG * G) * p.nco_inc);
+    float2 ea = nco_direct((uint32_t)(G * tid) * p.nco_inc);
+#pragma unroll
+    for (int b0 = 0; b0 < BPT; b0 += SB) {
+      float4 v[SB];
+      const float4* __restrict__ src = reinterpret_cast<const float4*>(in + S0);
+      if (whole) {
+#pragma unroll
+        for (int k = 0; k < SB; ++k) v[k] = load16_nt(src + (b0 + k) * WG + tid);
+      } else {
+#pragma unroll
+        for (int k = 0; k < SB; ++k) v[k] = load_granule<InT, VEC>(in, S0 + (uint64_t)((b0 + k) * WG + tid) * G, p.L);
+      }
+#pragma unroll
+      for (int k = 0; k < SB; ++k) {
+        if (b0 + k > 0) ea = cmul(ea, F);
+        const float2 eb = cmul(ea, w);
+        const float2 a = cmul(make_float2(v[k].x, v[k].y), ea);
+        const float2 b = cmul(make_float2(v[k].z, v[k].w), eb);
+        lds[pbase + (uint32_t)(b0 + k) * Geo::padded(WG)] = make_float4(a.x, a.y, b.x, b.y);
+      }
+    }
+    for (uint32_t g = BPT * WG + tid; g < NG; g += WG) {
+      ea = cmul(ea, F);
+      const float4 v = load_granule<InT, VEC>(in, S0 + (uint64_t)g * G, p.L);
+      const float2 eb = cmul(ea, w);
+      const float2 a = cmul(make_float2(v.x, v.y), ea);
+      const float2 b = cmul(make_float2(v.z, v.w), eb);
+      lds[Geo::padded(g)] = make_float4(a.x, a.y, b.x, b.y);
+    }
+    return;
+  }
   auto body = [&](auto odd_c) {
     constexpr bool ODD = decltype(odd_c)::value;
 #pragma unroll
@@ -785,7 +879,7 @@ __device__ __forceinline__ void tile_epilogue(const FirParams& p, uint64_t out0,
 // Polyphase compute core shared by the polyphase kernels: thread t accumulates its R outputs from
 // the staged tile in LDS. JC = tap rows per chunk (a multiple of R); a chunk covers JC*D taps.
 // ------------------------------------------------------------------------------------------------
-template <class TapT, class InT, int D, int R, int JC, int WG>
+template <class TapT, class InT, int D, int R, int JC, int WG, bool LIGHT = false, bool FENCE = false>
 __device__ __forceinline__ void poly_compute(const float4* __restrict__ lds, const FirParams& p,
                                              typename Product<TapT, InT>::type (&acc)[R]) {
   using Geo = TileGeo<InT, D, R, WG>;
@@ -807,11 +901,20 @@ __device__ __forceinline__ void poly_compute(const float4* __restrict__ lds, con
 #pragma unroll
         for (int e = 0; e < G; ++e) tv[j][e] = tap_at<TapT>(tb, j * D + e);
       }
+      // FENCE: keeps one column's window reads from being scheduled ahead of the previous column's
+      // multiply-adds (the persistent kernel's scheduler otherwise held every window at once)
+      if constexpr (FENCE) asm volatile("" ::: "memory");
       float4 win[NWIN];
 #pragma unroll
       for (int u = 0; u < NWIN; ++u) {
         const int q = u * CPR + h;
-        win[u] = seg[q + Geo::PAD * (q / Geo::SG)];
+        // LIGHT (tuning probe, wrong results): only the thread's own R rows come from LDS, the rest of
+        // the window repeats them -- the same FMAs with 4/19 of the LDS reads
+        if (!LIGHT || u < R) {
+          win[u] = seg[q + Geo::PAD * (q / Geo::SG)];
+        } else {
+          win[u] = win[u - R];
+        }
       }
 #pragma unroll
       for (int j = 0; j < JC; ++j) {
@@ -933,7 +1036,8 @@ __device__ __forceinline__ bool all_finite(const float (&acc)[R]) {
 // Kernel 1: polyphase-granule kernel, one tile per workgroup (D a multiple of the granule width G).
 // ABL (ablation, tuning probes only): low bits 0 = full kernel, 1 = staging only, 2 = compute only;
 // chain-mode flags 8 = staging without the NCO mix, 16 = plain float store instead of the FM
-// discriminator, 32 = NCO mix without the per-granule transcendental pair.
+// discriminator, 32 = NCO mix without the per-granule transcendental pair, 128 = tile-relative phasors
+// by recurrence; 64 = register window from the thread's own R rows only (wrong results: LDS-read probe).
 // NT: non-temporal (streaming) HBM loads for the staged input.
 // ------------------------------------------------------------------------------------------------
 // Tile of workgroup b. XCD-aware (XM): workgroups are dispatched round-robin over the 8 XCDs, so
@@ -961,6 +1065,7 @@ __device__ __forceinline__ void fir_poly_tile(const FirParams& p, uint32_t tile)
 
   extern __shared__ __attribute__((aligned(16))) float4 lds[];
   const InT* __restrict__ in = reinterpret_cast<const InT*>(p.in);
+  stream_copy_history<InT>(p);
 
   const uint64_t out0 = (uint64_t)tile * p.tile_stride;
   const uint64_t S0 = out0 * D;
@@ -968,7 +1073,9 @@ __device__ __forceinline__ void fir_poly_tile(const FirParams& p, uint32_t tile)
   const uint32_t NG = ((Geo::KT - 1) * D + span + G - 1) / G;
   // LDS: [tile granules | FM exchange (WG float2)]
   constexpr int SMODE = (ABL & 8) ? (int)kModeFir : MODE;
-  if constexpr ((ABL & 7) != 2) stage_tile<InT, Geo, WG, VEC, SMODE, NT, DMA, SH, (ABL & 32) != 0>(lds, in, S0, NG, p);
+  if constexpr ((ABL & 7) != 2) {
+    stage_tile<InT, Geo, WG, VEC, SMODE, NT, DMA, SH, (ABL & 32) != 0, (ABL & 128) != 0>(lds, in, S0, NG, p);
+  }
   __syncthreads();
 
   OutT acc[R];
@@ -979,8 +1086,8 @@ __device__ __forceinline__ void fir_poly_tile(const FirParams& p, uint32_t tile)
 #pragma unroll
     for (int r = 0; r < R; ++r) mac(acc[r], granule_sample<typename LdsSample<InT>::type>(v, r % G), 1.0f);
   } else {
-    poly_compute<TapT, InT, D, R, JC, WG>(lds, p, acc);
-    if constexpr (ABL == 0) {
+    poly_compute<TapT, InT, D, R, JC, WG, (ABL & 64) != 0>(lds, p, acc);
+    if constexpr ((ABL & ~128) == 0) {
       if (!all_finite(acc)) poly_fixup<TapT, InT, D, R, JC, WG>(lds, p, acc);
     }
   }
@@ -1005,6 +1112,81 @@ template <class TapT, class InT, int D, int R, int JC, int WG, bool VEC, int MOD
           bool XM = false, int CST = 0, bool DMA = false, int SH = 0>
 __global__ __launch_bounds__(WG) void k_fir_poly(FirParams p) {
   fir_poly_tile<TapT, InT, D, R, JC, WG, VEC, MODE, ABL, NT, CST, DMA, SH>(p, tile_of_block<XM>());
+}
+
+// ------------------------------------------------------------------------------------------------
+// Kernel 1p (tuning probe): FM / AM chain on persistent workgroups whose NCO phasors are tile-relative
+// and held in registers: granule k * WG + tid of every tile starts at tile-relative sample
+// G (k WG + tid), so its two phasors are the same for every tile and are computed once per workgroup.
+// The discriminator and the envelope are invariant to the rotation this leaves common to a tile.
+// ------------------------------------------------------------------------------------------------
+template <class TapT, class InT, int D, int R, int JC, int WG, int MODE>
+__global__ __launch_bounds__(WG) void k_fir_poly_rel(FirParams p, uint32_t ntiles) {
+  using Geo = TileGeo<InT, D, R, WG>;
+  using OutT = typename Product<TapT, InT>::type;
+  constexpr int G = Geo::G;
+  static_assert(G == 2 && MODE != kModeFir, "complex chains");
+  constexpr int BPT = Geo::SG * (Geo::KT / Geo::ROUT) / WG;
+  extern __shared__ __attribute__((aligned(16))) float4 lds[];
+  const InT* __restrict__ in = reinterpret_cast<const InT*>(p.in);
+  const uint32_t span = p.nch * JC * D;
+  const uint32_t NG = ((Geo::KT - 1) * D + span + G - 1) / G;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t pbase = Geo::padded(tid);
+  float4 ph[BPT + 1];
+#pragma unroll
+  for (int k = 0; k <= BPT; ++k) {
+    const uint32_t s = (uint32_t)G * ((uint32_t)k * WG + tid);
+    const float2 a = nco_direct(s * p.nco_inc), b = nco_direct((s + 1u) * p.nco_inc);
+    ph[k] = make_float4(a.x, a.y, b.x, b.y);
+  }
+  for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    __syncthreads();  // the previous tile's epilogue is done with LDS
+    const uint64_t out0 = (uint64_t)tile * p.tile_stride;
+    const uint64_t S0 = out0 * D;
+    const bool whole = S0 + (uint64_t)NG * G <= p.L;
+    float4 v[BPT + 1];
+    const float4* __restrict__ src = reinterpret_cast<const float4*>(in + S0);
+    const uint32_t gh = BPT * WG + tid;
+    if (whole) {
+#pragma unroll
+      for (int k = 0; k < BPT; ++k) v[k] = load16_nt(src + k * WG + tid);
+      if (gh < NG) v[BPT] = load16_nt(src + gh);
+    } else {
+#pragma unroll
+      for (int k = 0; k < BPT; ++k) v[k] = load_granule<InT, false>(in, S0 + (uint64_t)(k * WG + tid) * G, p.L);
+      if (gh < NG) v[BPT] = load_granule<InT, false>(in, S0 + (uint64_t)gh * G, p.L);
+    }
+#pragma unroll
+    for (int k = 0; k < BPT; ++k) {
+      const float2 a = cmul(make_float2(v[k].x, v[k].y), make_float2(ph[k].x, ph[k].y));
+      const float2 b = cmul(make_float2(v[k].z, v[k].w), make_float2(ph[k].z, ph[k].w));
+      lds[pbase + (uint32_t)k * Geo::padded(WG)] = make_float4(a.x, a.y, b.x, b.y);
+    }
+    if (gh < NG) {
+      const float2 a = cmul(make_float2(v[BPT].x, v[BPT].y), make_float2(ph[BPT].x, ph[BPT].y));
+      const float2 b = cmul(make_float2(v[BPT].z, v[BPT].w), make_float2(ph[BPT].z, ph[BPT].w));
+      lds[Geo::padded(gh)] = make_float4(a.x, a.y, b.x, b.y);
+    }
+    for (uint32_t g = gh + WG; g < NG; g += WG) {  // halo beyond one row of granules (large tap counts)
+      const float4 w = load_granule<InT, false>(in, S0 + (uint64_t)g * G, p.L);
+      const float2 a = cmul(make_float2(w.x, w.y), nco_direct((uint32_t)G * g * p.nco_inc));
+      const float2 b = cmul(make_float2(w.z, w.w), nco_direct(((uint32_t)G * g + 1u) * p.nco_inc));
+      lds[Geo::padded(g)] = make_float4(a.x, a.y, b.x, b.y);
+    }
+    __syncthreads();
+    OutT acc[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) set_zero(acc[r]);
+    // the taps are loop-invariant: hoisted out of the tile loop they held ~128 VGPRs (they do not fit
+    // the SGPRs), so their address is made opaque per tile and the scalar loads stay in the core
+    FirParams pt = p;
+    asm volatile("" : "+s"(pt.taps));
+    poly_compute<TapT, InT, D, R, JC, WG, false, true>(lds, pt, acc);
+    if (!all_finite(acc)) poly_fixup<TapT, InT, D, R, JC, WG>(lds, pt, acc);
+    float2* xs = reinterpret_cast<float2*>(lds + Geo::padded(NG - 1) + 1);
+    tile_epilogue<MODE, OutT, R, WG, true, true>(p, out0, acc, xs, lds);
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1055,6 +1237,7 @@ __global__ __launch_bounds__(WG) void k_fir_contig(FirParams p) {
 
   extern __shared__ __attribute__((aligned(16))) float4 lds[];
   const InT* __restrict__ in = reinterpret_cast<const InT*>(p.in);
+  stream_copy_history<InT>(p);
 
   const uint64_t out0 = (uint64_t)blockIdx.x * p.tile_stride;
   const uint64_t S0 = out0 * D;

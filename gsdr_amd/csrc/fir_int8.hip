@@ -64,4 +64,30 @@ hipError_t fir_int8_stream_step(uint64_t outputIndex, const float* taps, size_t 
   if (scope.status() != hipSuccess) return scope.status();
   return launch_i8_mfma<4, 3>(job, stream);
 }
+
+// The same on the tiled kernels (decimations other than 4, or tap counts the matrix-core kernel does not
+// take): the exact path, as the monolithic call runs for those shapes (stream_step_tiled).
+hipError_t fir_int8_stream_step_tiled(size_t decimation, const float* taps, size_t tapCount, const int8_t* chunk,
+                                      uint64_t chunkLen, int64_t inOff, const int8_t* hist, uint64_t histLen,
+                                      int8_t* histOut, int64_t histFrom, uint64_t histN, hipFloatComplex* output,
+                                      size_t numOutputs, int32_t device, hipStream_t stream) {
+  FirJob job;
+  job.in = chunk;
+  job.taps = taps;
+  job.out = output;
+  job.D = decimation;
+  job.T = tapCount;
+  job.N = numOutputs;
+  job.L = chunkLen;
+  job.mode = kModeFir;
+  job.in_off = inOff;
+  job.hist = hist;
+  job.hist_len = histLen;
+  job.hist_out = histOut;
+  job.hist_from = histFrom;
+  job.hist_n = histN;
+  DeviceScope scope(device);
+  if (scope.status() != hipSuccess) return scope.status();
+  return stream_step_tiled<Iq8, kModeFir>(job, stream);
+}
 }  // namespace gsdr

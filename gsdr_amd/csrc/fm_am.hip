@@ -160,6 +160,40 @@ hipError_t chain_int8_stream_step(int mode, float fs, float tune, float chan, fl
   return mode == kModeFm ? launch_chain_i8_mfma<kModeFm>(job, stream) : launch_chain_i8_mfma<kModeAm>(job, stream);
 }
 
+// The streaming object's one-launch chain step on the tiled kernels (stream_step_tiled), complex float or
+// int8 I/Q chunks: firstSampleIndex is the absolute index of output 0's first sample.
+hipError_t chain_stream_step_tiled(int mode, bool int8, float fs, float tune, float chan, float dev, uint32_t decimation,
+                                   size_t firstSampleIndex, const float* taps, size_t tapCount, const void* chunk,
+                                   uint64_t chunkLen, int64_t inOff, const void* hist, uint64_t histLen, void* histOut,
+                                   int64_t histFrom, uint64_t histN, float* output, size_t numOutputs, int32_t device,
+                                   hipStream_t stream) {
+  FirJob job;
+  if (!nco_increment(fs, tune, chan, &job.nco_inc)) return hipErrorInvalidValue;
+  job.in = chunk;
+  job.taps = taps;
+  job.out = output;
+  job.D = decimation;
+  job.T = tapCount;
+  job.N = numOutputs;
+  job.L = chunkLen;
+  job.mode = mode;
+  job.nco_n0 = (uint32_t)firstSampleIndex;
+  if (mode == kModeFm) job.fm_gain = fs / (2.0f * kPiF * dev);
+  job.in_off = inOff;
+  job.hist = hist;
+  job.hist_len = histLen;
+  job.hist_out = histOut;
+  job.hist_from = histFrom;
+  job.hist_n = histN;
+  DeviceScope scope(device);
+  if (scope.status() != hipSuccess) return scope.status();
+  if (int8) {
+    return mode == kModeFm ? stream_step_tiled<Iq8, kModeFm>(job, stream) : stream_step_tiled<Iq8, kModeAm>(job, stream);
+  }
+  return mode == kModeFm ? stream_step_tiled<float2, kModeFm>(job, stream)
+                         : stream_step_tiled<float2, kModeAm>(job, stream);
+}
+
 }  // namespace gsdr
 
 GSDR_C_LINKAGE hipError_t gsdrFmDemod(float rfSampleRate, float tuningFrequency, float channelFrequency,

@@ -235,6 +235,9 @@ constexpr int kFusedMaxP = IIR_FUSED_MAXP;
 #ifndef IIR_PROBE_FINAL
 #define IIR_PROBE_FINAL 0
 #endif
+#if (IIR_PROBE_TAILS || IIR_PROBE_FINAL) && !defined(GSDR_TUNING_PROBES)
+#error "IIR_PROBE_TAILS / IIR_PROBE_FINAL produce wrong results (timing ablations): probe builds only"
+#endif
 
 struct ScanArgs {
   double* incl;          // level-0 inclusive zero-state prefixes (A[P] per chunk); tails pass writes

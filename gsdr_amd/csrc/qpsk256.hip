@@ -292,7 +292,7 @@ __global__ __launch_bounds__(kCBlock) void k_c256_mod_awgn(const uint8_t* __rest
     float2 y[kAwgnSym];
 #pragma unroll
     for (int j = 0; j < kAwgnSym; ++j) {
-      const float2 g = awgn_slot(ntab, w[(R3 + j) / 3], (R3 + j) % 3);
+      const float2 g = awgn_slot(ntab, w[(R3 + j) / 3], (R3 + j) % 3, seed, b0 + (R3 + j) / 3);
       const float2 p = tab[sym[j]];
       y[j] = make_float2(p.x + sigma * g.x, p.y + sigma * g.y);
     }

@@ -1,13 +1,17 @@
 // gsdr-mi355x: streaming continuity object (include/gsdr/stream.h).
 //
-// Host-side bookkeeping around the filter entry points. The reference has no equivalent: its callers
-// re-supply the overlap themselves (include/gsdr/fm.h:26, fm.cu:202). Per Process call:
-//   * seam outputs (window starts in the history, ends in the new chunk): history + chunk head are
-//     stitched into a small device buffer and filtered from there;
-//   * every other computable output is filtered straight from the caller's chunk;
-//   * the samples the next output still needs (< one window) become the new history.
-// Each launch passes the absolute index of its first sample as firstSampleIndex, so the NCO phase
-// and the kernel selection are those of one monolithic call: the outputs are bit-identical.
+// Host-side bookkeeping around the filter kernels. The reference has no equivalent: its callers
+// re-supply the overlap themselves (include/gsdr/fm.h:26, fm.cu:202), one launch per chunk. Per Process
+// call, ONE launch (round 4; the int8 matrix-core kernels since round 3):
+//   * seam outputs (window starts in the history, ends in the new chunk) read their first samples from
+//     the history buffer by offset, every other output straight from the caller's chunk;
+//   * workgroup 0 of the same launch copies the samples the next output still needs (< one window) into
+//     the spare history buffer (ping-pong).
+// The launch runs the kernel one monolithic call would run, with the absolute index of output 0's first
+// sample as firstSampleIndex, so the NCO phase and the per-output MAC order are those of that call: the
+// outputs are bit-identical. Shapes without a one-launch kernel (runtime-decimation and generic kernels)
+// keep the older plan: a gather launch (seam = history + chunk head, next history), then the seam and the
+// main outputs as two filter calls.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -48,6 +52,20 @@ hipError_t fir_int8_stream_step(uint64_t outputIndex, const float* taps, size_t 
                                 uint64_t chunkLen, int64_t inOff, const int8_t* hist, uint64_t histLen, int8_t* histOut,
                                 int64_t histFrom, uint64_t histN, hipFloatComplex* output, size_t numOutputs,
                                 int32_t device, hipStream_t stream);
+// the one-launch steps on the tiled kernels (fir_dispatch.hpp stream_step_tiled): fir.hip, fir_int8.hip, fm_am.hip
+hipError_t fir_fc_stream_step(size_t decimation, const float* taps, size_t tapCount, const hipFloatComplex* chunk,
+                              uint64_t chunkLen, int64_t inOff, const hipFloatComplex* hist, uint64_t histLen,
+                              hipFloatComplex* histOut, int64_t histFrom, uint64_t histN, hipFloatComplex* output,
+                              size_t numOutputs, int32_t device, hipStream_t stream);
+hipError_t fir_int8_stream_step_tiled(size_t decimation, const float* taps, size_t tapCount, const int8_t* chunk,
+                                      uint64_t chunkLen, int64_t inOff, const int8_t* hist, uint64_t histLen,
+                                      int8_t* histOut, int64_t histFrom, uint64_t histN, hipFloatComplex* output,
+                                      size_t numOutputs, int32_t device, hipStream_t stream);
+hipError_t chain_stream_step_tiled(int mode, bool int8, float fs, float tune, float chan, float dev, uint32_t decimation,
+                                   size_t firstSampleIndex, const float* taps, size_t tapCount, const void* chunk,
+                                   uint64_t chunkLen, int64_t inOff, const void* hist, uint64_t histLen, void* histOut,
+                                   int64_t histFrom, uint64_t histN, float* output, size_t numOutputs, int32_t device,
+                                   hipStream_t stream);
 // fm_am.hip (mode 1 = FM, 2 = AM as in fir_engine.hpp)
 hipError_t chain_int8_stream_step(int mode, float fs, float tune, float chan, float dev, size_t firstSampleIndex,
                                   const float* taps, size_t tapCount, const int8_t* chunk, uint64_t chunkLen,
@@ -226,22 +244,44 @@ GSDR_C_LINKAGE hipError_t gsdrxStreamProcess(gsdrxStream s, const void* input, s
   const uint64_t S = s->consumed, h0 = s->next_out * s->D;
   const uint64_t h = S > h0 ? S - h0 : 0;
   hipError_t e = hipSuccess;
-  if (s->format == GSDRX_SAMPLES_CS8 && s->D == 4 && n_out > 0) {
-    // int8 I/Q at decimation 4: ONE launch of the matrix-core kernel does the seam outputs (their samples
-    // before the chunk read from the history buffer), the direct outputs and the next history copy
+  if (n_out > 0) {
+    // ONE launch does the seam outputs (their samples before the chunk read from the history buffer), the
+    // direct outputs and the next history copy: the int8 matrix-core kernels at decimation 4, the tiled
+    // kernels otherwise (the same kernels as one monolithic call, tile for tile)
     const int64_t in_off = (int64_t)(s->next_out * s->D) - (int64_t)S;
     const int64_t from = (int64_t)(p.m_end * s->D) - (int64_t)S;
-    const int8_t* c8 = reinterpret_cast<const int8_t*>(chunk);
-    const int8_t* h8 = reinterpret_cast<const int8_t*>(s->hist);
-    int8_t* n8 = reinterpret_cast<int8_t*>(s->spare);
-    if (s->kind == GSDRX_STREAM_FIR) {
-      e = gsdr::fir_int8_stream_step(s->next_out, s->taps, s->T, c8, numInputSamples, in_off, h8, h, n8, from,
-                                     p.hist_after, reinterpret_cast<hipFloatComplex*>(out), n_out, s->device,
-                                     cudaStream);
-    } else {
-      e = gsdr::chain_int8_stream_step(s->kind == GSDRX_STREAM_FM ? 1 : 2, s->fs, s->tune, s->chan, s->dev,
-                                       s->n0 + h0, s->taps, s->T, c8, numInputSamples, in_off, h8, h, n8, from,
-                                       p.hist_after, reinterpret_cast<float*>(out), n_out, s->device, cudaStream);
+    const bool i8 = s->format == GSDRX_SAMPLES_CS8;
+    const int mode = s->kind == GSDRX_STREAM_FM ? 1 : 2;
+    e = hipErrorNotSupported;
+    if (i8 && s->D == 4) {
+      const int8_t* c8 = reinterpret_cast<const int8_t*>(chunk);
+      const int8_t* h8 = reinterpret_cast<const int8_t*>(s->hist);
+      int8_t* n8 = reinterpret_cast<int8_t*>(s->spare);
+      if (s->kind == GSDRX_STREAM_FIR) {
+        e = gsdr::fir_int8_stream_step(s->next_out, s->taps, s->T, c8, numInputSamples, in_off, h8, h, n8, from,
+                                       p.hist_after, reinterpret_cast<hipFloatComplex*>(out), n_out, s->device,
+                                       cudaStream);
+      } else {
+        e = gsdr::chain_int8_stream_step(mode, s->fs, s->tune, s->chan, s->dev, s->n0 + h0, s->taps, s->T, c8,
+                                         numInputSamples, in_off, h8, h, n8, from, p.hist_after,
+                                         reinterpret_cast<float*>(out), n_out, s->device, cudaStream);
+      }
+    }
+    if (e == hipErrorNotSupported) {
+      if (s->kind == GSDRX_STREAM_FIR) {
+        e = i8 ? gsdr::fir_int8_stream_step_tiled(s->D, s->taps, s->T, reinterpret_cast<const int8_t*>(chunk),
+                                                  numInputSamples, in_off, reinterpret_cast<const int8_t*>(s->hist), h,
+                                                  reinterpret_cast<int8_t*>(s->spare), from, p.hist_after,
+                                                  reinterpret_cast<hipFloatComplex*>(out), n_out, s->device, cudaStream)
+               : gsdr::fir_fc_stream_step(s->D, s->taps, s->T, reinterpret_cast<const hipFloatComplex*>(chunk),
+                                          numInputSamples, in_off, reinterpret_cast<const hipFloatComplex*>(s->hist), h,
+                                          reinterpret_cast<hipFloatComplex*>(s->spare), from, p.hist_after,
+                                          reinterpret_cast<hipFloatComplex*>(out), n_out, s->device, cudaStream);
+      } else {
+        e = gsdr::chain_stream_step_tiled(mode, i8, s->fs, s->tune, s->chan, s->dev, s->D, s->n0 + h0, s->taps, s->T,
+                                          chunk, numInputSamples, in_off, s->hist, h, s->spare, from, p.hist_after,
+                                          reinterpret_cast<float*>(out), n_out, s->device, cudaStream);
+      }
     }
     if (e == hipSuccess) {
       std::swap(s->hist, s->spare);

@@ -199,8 +199,11 @@ GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxAmDemodMulti(
  *     rounded, then the sum rounded (two roundings, no fused multiply-add),
  * where (g0, g1) are the standard normals of absolute symbol index firstSymbolIndex + k: 21 bits of
  * Philox4x32-10 keyed by `seed` per normal, mapped by inverse-CDF interpolation in a 672-entry
- * half-normal quantile table (within 2.5e-5 of the exact quantile, tails cut at 5.035; the exact
- * construction is in gsdr_amd/csrc/awgn.hpp and its host restatement in oracle/gsdr_oracle.h), built
+ * half-normal quantile table (within 2.5e-5 of the exact quantile); a component in the deep tail
+ * (|g| > 4.17, ~3e-5 of them) draws 18 more bits from a second Philox block and a 768-entry tail table,
+ * so the tails follow the Gaussian to within 1 % of its tail mass out to 6.5 and reach 7.0 (P(|g| > 7) =
+ * 2.6e-12 per axis is the only mass missing: SER / BER sweeps are unbiased above ~1e-10). The exact
+ * construction is in gsdr_amd/csrc/awgn.hpp and its host restatement in oracle/gsdr_oracle.h, built
  * from exact integer operations and one correctly rounded fmaf. The noise
  * is therefore a pure function of (seed, absolute index): a host can regenerate the noisy buffer bit
  * for bit, and splitting a buffer over several calls (advancing firstSymbolIndex) yields the same

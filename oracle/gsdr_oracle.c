@@ -510,21 +510,62 @@ float oracle_awgn_normal21(uint32_t r) {
   return f_from_bits(f_bits(m) ^ ((r << 11) & 0x80000000u));
 }
 
+/* The tail extension (awgn.hpp, round 4): a component with a = r & 0xfffff < 32 takes 18 more bits e,
+ * x' = 2 (a 2^18 + e) + 1 < 2^24 (exact in float), v' = x' 2^-39, read from the 24 x 32 tail table the
+ * same way as the main table. */
+static const float awgn_tail_table[24 * 32][2] = {
+#define GSDR_AWGN_ENTRY(r, s) {r, s},
+#include "../gsdr_amd/csrc/awgn_tail_table.inc"
+#undef GSDR_AWGN_ENTRY
+};
+
+float oracle_awgn_tail_normal(uint32_t r, uint32_t e) {
+  const uint32_t x = ((((r & 0x1fu) << 18) | (e & 0x3ffffu)) << 1) | 1u;
+  const uint32_t b = f_bits((float)x);
+  const uint32_t i = (b >> 18) - 127u * 32u;
+  const float f = (float)(b & 0x3ffffu) * 3.814697265625e-06f;
+  const float m = fmaf(awgn_tail_table[i][1] * 262144.0f, f, awgn_tail_table[i][0]);
+  return f_from_bits(f_bits(m) ^ ((r << 11) & 0x80000000u));
+}
+
+static int awgn_in_tail(uint32_t r) { return (r & 0xfffe0u) == 0u; }
+
 /* symbol k: Philox block k / 3 (counter (blk lo, blk hi, 0, 0), key = seed), slot k % 3, 21 bits a
- * component (gsdr_amd/csrc/awgn.hpp) */
+ * component; a component in the tail (a < 32) takes 18 bits of the extension block (counter
+ * (blk lo, blk hi, 1, 0)) as gsdr_amd/csrc/awgn.hpp documents */
 void oracle_awgn_normals(uint64_t seed, uint64_t symbol_index, float* g0, float* g1) {
   const uint64_t blk = symbol_index / 3u;
   const uint32_t ctr[4] = {(uint32_t)blk, (uint32_t)(blk >> 32), 0u, 0u};
   const uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
   uint32_t w[4];
   oracle_philox4x32_10(ctr, key, w);
-  switch ((int)(symbol_index % 3u)) {
-    case 0: *g0 = oracle_awgn_normal21(w[0] >> 11); *g1 = oracle_awgn_normal21(w[1] >> 11); break;
-    case 1: *g0 = oracle_awgn_normal21(w[2] >> 11); *g1 = oracle_awgn_normal21(w[3] >> 11); break;
+  const int slot = (int)(symbol_index % 3u);
+  uint32_t r0, r1;
+  switch (slot) {
+    case 0: r0 = w[0] >> 11; r1 = w[1] >> 11; break;
+    case 1: r0 = w[2] >> 11; r1 = w[3] >> 11; break;
     default:
-      *g0 = oracle_awgn_normal21(((w[0] & 0x7ffu) << 10) | ((w[1] & 0x7ffu) >> 1));
-      *g1 = oracle_awgn_normal21(((w[2] & 0x7ffu) << 10) | ((w[3] & 0x7ffu) >> 1));
+      r0 = ((w[0] & 0x7ffu) << 10) | ((w[1] & 0x7ffu) >> 1);
+      r1 = ((w[2] & 0x7ffu) << 10) | ((w[3] & 0x7ffu) >> 1);
       break;
+  }
+  *g0 = oracle_awgn_normal21(r0);
+  *g1 = oracle_awgn_normal21(r1);
+  if (awgn_in_tail(r0) || awgn_in_tail(r1)) {
+    const uint32_t ctr1[4] = {(uint32_t)blk, (uint32_t)(blk >> 32), 1u, 0u};
+    uint32_t x[4];
+    oracle_philox4x32_10(ctr1, key, x);
+    uint32_t e0, e1;
+    switch (slot) {
+      case 0: e0 = x[0] >> 14; e1 = x[1] >> 14; break;
+      case 1: e0 = x[2] >> 14; e1 = x[3] >> 14; break;
+      default:
+        e0 = ((x[0] & 0x3fffu) << 4) | (x[2] & 0xfu);
+        e1 = ((x[1] & 0x3fffu) << 4) | (x[3] & 0xfu);
+        break;
+    }
+    if (awgn_in_tail(r0)) *g0 = oracle_awgn_tail_normal(r0, e0);
+    if (awgn_in_tail(r1)) *g1 = oracle_awgn_tail_normal(r1, e1);
   }
 }
 

@@ -115,9 +115,13 @@ void oracle_qpsk256_demod_cuabs(const float* table, const float* in, uint8_t* ou
  * (w0 & 0x7ff) << 10 | (w1 & 0x7ff) >> 1, (w2 & 0x7ff) << 10 | (w3 & 0x7ff) >> 1). A component's bits
  * give a sign and the tail probability v = (2a + 1) 2^-21; |g| is the half-normal quantile -Phi^-1(v/2)
  * by linear interpolation in a 21 x 32 table (gsdr_amd/csrc/awgn_table.inc; one fmaf), so the device
- * and the host round identically. Output = fl(table[s] + fl(sigma g)) per component (no FMA). */
+ * and the host round identically. A component with a < 32 (|g| > 4.17) takes 18 more bits from the
+ * extension block (counter (block lo, hi, 1, 0)) and the 24 x 32 tail table (awgn_tail_table.inc), so the
+ * tails reach 7.0 instead of 5.035. Output = fl(table[s] + fl(sigma g)) per component (no FMA). */
 void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
 float oracle_awgn_normal21(uint32_t r);
+/* tail extension: a = r & 0xfffff < 32 with 18 more bits e (gsdr_amd/csrc/awgn.hpp) */
+float oracle_awgn_tail_normal(uint32_t r, uint32_t e);
 void oracle_awgn_normals(uint64_t seed, uint64_t symbol_index, float* g0, float* g1);
 void oracle_qpsk256_mod_awgn(const float* table, const uint8_t* in, float* out, uint32_t n, float sigma,
                              uint64_t seed, uint64_t first_symbol);

@@ -66,6 +66,8 @@ _lib.oracle_cuCabsf.argtypes = [_f, _f]
 _lib.oracle_cuCabsf.restype = _f
 _lib.oracle_awgn_normal21.argtypes = [_u32]
 _lib.oracle_awgn_normal21.restype = _f
+_lib.oracle_awgn_tail_normal.argtypes = [_u32, _u32]
+_lib.oracle_awgn_tail_normal.restype = _f
 _lib.oracle_nco_inc.restype = _u32
 
 
@@ -245,6 +247,11 @@ def philox4x32_10(ctr, key):
 def awgn_normal21(bits):
     """One standard normal from 21 random bits (the AWGN construction, gsdr_amd/csrc/awgn.hpp)."""
     return float(_lib.oracle_awgn_normal21(bits))
+
+
+def awgn_tail_normal(bits, ext):
+    """The tail extension of a component whose 20-bit a is below 32: 18 more bits `ext` (awgn.hpp)."""
+    return float(_lib.oracle_awgn_tail_normal(bits, ext))
 
 
 def awgn_normals(seed, symbol_index):

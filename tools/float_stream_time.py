@@ -1,5 +1,6 @@
 """Per-call cost of short float calls (development tool): config 2's complex64 channel through a gsdrxStream
-(CF32 FIR, D = 4) in 1 / 8 / 32 / 128 chunks a pass, against one gsdrFirFC call (HIP events)."""
+(CF32 FIR, D = 4; then the FM chain) in 1 / 8 / 32 / 128 chunks a pass, against one gsdrFirFC / gsdrFmDemod
+call (HIP events)."""
 import ctypes
 import os
 import sys
@@ -40,15 +41,22 @@ def timed(fn, args, reps):
 res = ["gsdrFirFC %.1f" % timed(abi.lib.gsdrFirFC, [(D, taps.data_ptr(), T, x.data_ptr(), y.data_ptr(), N_OUT, 0, stream)
                                                     for x in xs], 60)]
 written = ctypes.c_size_t()
-for chunks in (1, 8, 32, 128):
-    h = ctypes.c_void_p()
-    assert abi.lib.gsdrxStreamCreate(ctypes.byref(h), 0, 0, D, taps.data_ptr(), T, 1.0, 0.0, 0.0, 1.0, 0, 0) == 0
-    cs = N_IN // chunks
-    args = []
-    for x in xs:
-        for c in range(chunks):
-            n = cs if c < chunks - 1 else N_IN - cs * (chunks - 1)
-            args.append((h, x.data_ptr() + 8 * cs * c, n, y.data_ptr(), y.numel(), ctypes.byref(written), stream))
-    res.append("stream x%d %.1f" % (chunks, timed(abi.lib.gsdrxStreamProcess, args, 20 * chunks) * chunks))
-    abi.lib.gsdrxStreamDestroy(h)
+f = ctypes.c_float
+N_FM = (N_IN - T) // D
+res.append("gsdrFmDemod %.1f" % timed(abi.lib.gsdrFmDemod, [(f(1e6), f(0.0), f(1e5), f(2e4), D, 0, taps.data_ptr(), T,
+                                                             x.data_ptr(), y.data_ptr(), N_FM, 0, stream) for x in xs], 60))
+for kind in (0, 1):
+    for chunks in (1, 8, 32, 128):
+        h = ctypes.c_void_p()
+        assert abi.lib.gsdrxStreamCreate(ctypes.byref(h), kind, 0, D, taps.data_ptr(), T, f(1e6), f(0.0), f(1e5),
+                                         f(2e4), 0, 0) == 0
+        cs = N_IN // chunks
+        args = []
+        for x in xs:
+            for c in range(chunks):
+                n = cs if c < chunks - 1 else N_IN - cs * (chunks - 1)
+                args.append((h, x.data_ptr() + 8 * cs * c, n, y.data_ptr(), y.numel(), ctypes.byref(written), stream))
+        res.append("%s stream x%d %.1f" % ("fir" if kind == 0 else "fm", chunks,
+                                           timed(abi.lib.gsdrxStreamProcess, args, 20 * chunks) * chunks))
+        abi.lib.gsdrxStreamDestroy(h)
 print(" | ".join(res), "(us per channel pass)")

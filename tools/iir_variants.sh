@@ -9,7 +9,7 @@ mkdir -p build/iirexp
 others=$(ls build/*.o | grep -v '/iir.o$')
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
-  ( /opt/rocm/bin/hipcc $HIPFLAGS $flags -c gsdr_amd/csrc/iir.hip -o build/iirexp/iir_$name.o &&
+  ( /opt/rocm/bin/hipcc $HIPFLAGS -DGSDR_TUNING_PROBES $flags -c gsdr_amd/csrc/iir.hip -o build/iirexp/iir_$name.o &&
     /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -Wl,-rpath,/opt/rocm/lib $others build/iirexp/iir_$name.o \
       -o build/iirexp/lib$name.so && echo "built $name" ) &
 done

@@ -433,8 +433,9 @@ inline hipError_t launch_d4_int8(const FirJob& j, hipStream_t s) {
       return launch_poly<float, Iq8, 4, 4, 16, 64, kModeFir, 0, true>(j, s);
     case 28:
       return launch_poly<float, Iq8, 4, 4, 16, 128, kModeFir, 0, true>(j, s);
-    case 40:  // matrix cores (exact bf16 tap parts, normwise parity), 4 workgroups per CU
-      return launch_i8_mfma<4, 4>(j, s);
+    case 40:  // matrix cores (exact bf16 tap parts, normwise parity), 2 workgroups per CU (round 2: 4, which the
+              // round-4 conflict-free LDS layout, 41 KB a workgroup, no longer fits)
+      return launch_i8_mfma<4, 2>(j, s);
     case 41:  // matrix cores, 3 workgroups per CU: the default for D = 4
       return launch_i8_mfma<4, 3>(j, s);
     case 42:  // matrix cores, 3 workgroups per CU, 1,024-output tiles at every size (tile-shape sweep)
@@ -471,6 +472,25 @@ template <class TapT, class InT, int D, int R, int JC, int WG, int MODE>
 hipError_t launch_poly_default(const FirJob& j, hipStream_t s) {
   static_assert(fits_lds_at_t127<InT, D, R, JC, WG>(), "default polyphase shape exceeds the LDS budget");
   return launch_poly<TapT, InT, D, R, JC, WG, MODE, 0, true>(j, s);
+}
+
+// Decimation 4 (the headline shape, complex or int8 I/Q samples) with the tile sized to the call: the
+// 1,024-output tiles (WG 256, R 4) measured fastest for a whole channel, but a short call (a stream chunk)
+// of fewer tiles than two rounds of workgroup slots is one tile's latency on part of the chip; 512- and
+// 256-output tiles (WG 128 / 64, same R and JC) put more of the chip on it. The per-output MAC order
+// depends only on (D, JC), so every tile size gives the same outputs bit for bit.
+template <class TapT, class InT, int MODE>
+hipError_t launch_poly_d4(const FirJob& j, hipStream_t s) {
+  int cus = 0;
+  if (current_device_cus(&cus) == hipSuccess && cus > 0) {
+    const uint64_t slots = (uint64_t)cus * 4;  // 38 KB tiles: 4 workgroups a CU
+    const uint64_t t256 = ceil_div<uint64_t>(j.N, 1024);
+    if (t256 < 2 * slots) {
+      if (ceil_div<uint64_t>(j.N, 512) >= 2 * slots) return launch_poly<TapT, InT, 4, 4, 16, 128, MODE, 0, true>(j, s);
+      return launch_poly<TapT, InT, 4, 4, 16, 64, MODE, 0, true>(j, s);
+    }
+  }
+  return launch_poly_default<TapT, InT, 4, 4, 16, 256, MODE>(j, s);
 }
 
 // Runtime-decimation tile kernel (k_fir_rt) for decimations without a compile-time shape, when taps
@@ -616,7 +636,7 @@ hipError_t launch_fir(const FirJob& j, hipStream_t s) {
       case 2:
         return launch_poly_default<TapT, InT, 2, 8, 16, 128, MODE>(j, s);
       case 4:
-        return launch_poly_default<TapT, InT, 4, 4, 16, 256, MODE>(j, s);
+        return launch_poly_d4<TapT, InT, MODE>(j, s);
       case 8:
         return launch_poly_default<TapT, InT, 8, 2, 8, 256, MODE>(j, s);
       default:
@@ -632,8 +652,9 @@ hipError_t launch_fir(const FirJob& j, hipStream_t s) {
         if constexpr (MODE == kModeFir && std::is_same<TapT, float>::value) {
           if (j.variant >= 0) return launch_d4_complex<TapT, InT, MODE>(j, s);
         }
-        // 4 waves/SIMD (16 per CU): the shape that measured fastest at T = 127
-        return launch_poly_default<TapT, InT, 4, 4, 16, 256, MODE>(j, s);
+        // 4 waves/SIMD (16 per CU): the shape that measured fastest at T = 127; smaller tiles
+        // for short calls
+        return launch_poly_d4<TapT, InT, MODE>(j, s);
       case 8:
         return launch_poly_default<TapT, InT, 8, 2, 8, 256, MODE>(j, s);
       default:

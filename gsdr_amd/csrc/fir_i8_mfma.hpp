@@ -148,8 +148,16 @@ struct I8OutScale {
   __device__ __forceinline__ float operator()(float acc) const { return ldexpf(acc * k, sh); }
 };
 
-// LDS plane layout: 2 bytes a sample, a 16-byte pad after every 64 samples
-__host__ __device__ constexpr uint32_t i8_addr(uint32_t idx) { return idx * 2u + (idx / 64u) * 16u; }
+// LDS plane layout: 2 bytes a sample, a 16-byte pad after every P samples. P is chosen per kernel so the
+// B-fragment reads (ds_read_b128, 16 lanes a cycle in the lane groups of MI355X_MICROARCH.md section LDS) hit
+// 16 distinct 16-byte bank slots, with the Q plane 128 bytes (mod 256) past the I plane: P = 32 for the FIR
+// kernel (lanes 16 b + 4 q' outputs apart), P = 16 for the chain kernel (8 b). Round 3's P = 64 for both
+// took 2x (FIR) and 2.5x (chain) the conflict-free LDS cycles (PMC: 42 % of the chain's LDS-active cycles
+// were bank conflicts, profiles/r04_pmc_kernels.txt).
+template <uint32_t P>
+__host__ __device__ constexpr uint32_t i8_addr(uint32_t idx) {
+  return idx * 2u + (idx / P) * 16u;
+}
 
 // Staging of samples [S0, S0 + SPAN) (absolute offsets into `in`, zero outside [0, L)) as bf16 I and Q
 // planes, in two halves so the next tile's loads can be in flight while this tile is computed (the
@@ -258,15 +266,16 @@ __device__ __forceinline__ void i8_load_granules(I8Stage<G, SPAN, WG>& st, const
   }
 }
 
-template <int G, int SPAN, int WG>
+template <uint32_t P, int G, int SPAN, int WG>
 __device__ __forceinline__ void i8_store_planes(const I8Stage<G, SPAN, WG>& st, char* lds, uint32_t plane) {
   using S = I8Stage<G, SPAN, WG>;
+  static_assert(P % G == 0, "a granule never straddles a pad");
   const uint32_t tid = threadIdx.x;
 #pragma unroll
   for (uint32_t r = 0; r < S::NGR; ++r) {
     const uint32_t g = tid + r * WG;
     if (g < S::NG) {
-      const uint32_t o = i8_addr(G * g);
+      const uint32_t o = i8_addr<P>(G * g);
       if constexpr (G == 8) {
         gsdr_b8 hi_, hq_;
 #pragma unroll
@@ -305,7 +314,8 @@ struct I8Mfma {
   static constexpr int MAXT = 32 * MAXNS - 15 * D;
   static constexpr int SPAN = (KT - 16) * D + 32 * MAXNS;  // samples staged per tile
   static_assert(SPAN % 8 == 0, "staging moves 8 samples a lane");
-  __host__ __device__ static constexpr uint32_t addr(uint32_t idx) { return i8_addr(idx); }
+  static constexpr uint32_t PADP = 32;  // pad period (i8_addr)
+  __host__ __device__ static constexpr uint32_t addr(uint32_t idx) { return i8_addr<PADP>(idx); }
   // Q plane offset: = 128 (mod 256), so the Q columns' bank groups interleave the I columns'
   static constexpr uint32_t PLANE = (addr(SPAN) + 255u) / 256u * 256u + 128u;
   static constexpr uint32_t LDS_BYTES = PLANE + addr(SPAN);
@@ -380,7 +390,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
   if (blockIdx.x < tiles) i8_load_granules<G, LM>(st, p, ((int64_t)blockIdx.x * C::KT - phase) * D + p.in_off);
   for (uint32_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
     const int64_t k_t = (int64_t)tile * C::KT - phase;  // a multiple of 16 in absolute output index
-    i8_store_planes(st, lds, C::PLANE);
+    i8_store_planes<C::PADP>(st, lds, C::PLANE);
     __syncthreads();
     // the next tile's loads fly while this one is computed
     if (tile + gridDim.x < tiles) {
@@ -454,7 +464,8 @@ struct I8ChainMfma {
   static constexpr int MAXT = 32 * MAXNS - 7 * D;  // 132
   static constexpr int SPAN = (KT - 8) * D + 32 * MAXNS;
   static_assert(SPAN % 4 == 0, "whole granules");
-  __host__ __device__ static constexpr uint32_t addr(uint32_t idx) { return i8_addr(idx); }
+  static constexpr uint32_t PADP = 16;  // pad period (i8_addr)
+  __host__ __device__ static constexpr uint32_t addr(uint32_t idx) { return i8_addr<PADP>(idx); }
   static constexpr uint32_t PLANE = (addr(SPAN) + 255u) / 256u * 256u + 128u;
   static constexpr uint32_t LDS_BYTES = PLANE + addr(SPAN);
 };
@@ -554,7 +565,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
   if (blockIdx.x < tiles) i8_load_granules<4, LM>(st, p, ((int64_t)blockIdx.x * C::STRIDE - phase) * D + p.in_off);
   for (uint32_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
     const int64_t k_t = (int64_t)tile * C::STRIDE - phase;  // a multiple of 16 in absolute output index
-    i8_store_planes(st, lds, C::PLANE);
+    i8_store_planes<C::PADP>(st, lds, C::PLANE);
     __syncthreads();
     // the next tile's loads fly while this one is computed
     if (tile + gridDim.x < tiles) {

@@ -84,7 +84,7 @@ GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxFirFCInt8(
     hipStream_t cudaStream) GSDR_NO_EXCEPT;
 
 /** gsdrxFirFCInt8 with an explicit decimation-4 tile shape (tuning sweep; -1 = default; 40 / 41 = the
- *  matrix-core kernel at 4 / 3 workgroups per CU; 42 / 43 = at 3 workgroups per CU with 1,024- / 512-output
+ *  matrix-core kernel at 2 / 3 workgroups per CU; 42 / 43 = at 3 workgroups per CU with 1,024- / 512-output
  *  tiles at every size, tapCount <= 132). */
 GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxFirFCInt8Variant(
     int variant,

@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""A few launches of each round-4 profiling target (development tool, for tools/pmc_cmd.sh): config 3 from
+int8 I/Q (gsdrxFmDemodInt8), config 5's channel and rectangular demodulation (2^24 symbols), and config 3's
+float FM chain. Prints the mean launch time of each (HIP events)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from gsdr_amd import ops  # noqa: E402
+from gsdr_amd.signals import lowpass_taps  # noqa: E402
+
+REPS = int(os.environ.get("REPS", "5"))
+dev = torch.device("cuda", 0)
+D, T, N_IN = 4, 127, 67_108_987
+n_fm = (N_IN - T) // D
+taps = torch.from_numpy(lowpass_taps(T, 0.1)).to(dev)
+g = torch.Generator(device=dev).manual_seed(1)
+x8 = torch.randint(-128, 128, (2 * N_IN,), dtype=torch.int8, device=dev, generator=g)
+xf = (torch.rand(2 * N_IN, device=dev, generator=g) * 2 - 1).view(torch.complex64)
+out = torch.empty(n_fm, dtype=torch.float32, device=dev)
+n = 1 << 24
+syms = torch.randint(0, 256, (n,), dtype=torch.uint8, device=dev, generator=g)
+rx = torch.empty(n, dtype=torch.complex64, device=dev)
+dec = torch.empty(n, dtype=torch.uint8, device=dev)
+ops.qpsk256_init(0, 1.0, 0)
+
+
+def timed(name, fn):
+    for _ in range(2):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(REPS):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    print(f"{name}: {e0.elapsed_time(e1) / REPS * 1e3:.1f} us", flush=True)
+
+
+timed("fm_chain_int8", lambda: ops.fm_demod(x8, taps, 1e6, 0.0, 1e5, 2e4, D, 0, n_fm, out=out))
+timed("qpsk256_mod_awgn", lambda: ops.qpsk256_modulate_awgn(syms, 0, 0.02, 0x5EED0005, 0, out=rx))
+timed("qpsk256_demod_rect", lambda: ops.qpsk256_demodulate(rx, 0, out=dec))
+timed("qpsk256_mod", lambda: ops.qpsk256_modulate(syms, 0, 1.0, out=rx))
+timed("fm_chain", lambda: ops.fm_demod(xf, taps, 1e6, 0.0, 1e5, 2e4, D, 0, n_fm, out=out))

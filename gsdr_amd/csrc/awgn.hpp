@@ -86,19 +86,45 @@ __device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t
   w[3] = c3;
 }
 
-// The table into LDS (all threads of the workgroup; the caller's barrier publishes it).
-__device__ __forceinline__ void awgn_load_table(float2* lds, uint32_t nthreads) {
-  for (uint32_t i = threadIdx.x; i < (uint32_t)kAwgnTableSize; i += nthreads) lds[i] = c_awgn_table[i];
+// The table in LDS as two float planes R and S (all threads of the workgroup; the caller's barrier
+// publishes it): a normal's two loads then land in any registers, where (R, S) pairs had to be shuffled
+// apart for the packed fma of a symbol's two normals (three moves a symbol).
+struct AwgnLds {
+  float r[kAwgnTableSize], s[kAwgnTableSize];
+};
+__device__ __forceinline__ void awgn_load_table(AwgnLds& t, uint32_t nthreads) {
+  for (uint32_t i = threadIdx.x; i < (uint32_t)kAwgnTableSize; i += nthreads) {
+    const float2 e = c_awgn_table[i];
+    t.r[i] = e.x;
+    t.s[i] = e.y;
+  }
+}
+
+// m with its sign flipped where bit 31 of `sgn` is set: one v_bitop3_b32 (m ^ (sgn & 0x80000000))
+__device__ __forceinline__ float awgn_sign(float m, uint32_t sgn) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x78" : "=v"(r) : "v"(__float_as_uint(m)), "v"(sgn), "s"(0x80000000u));
+  return __uint_as_float(r);
+}
+
+// One standard normal from a 20-bit a and a sign (bit 31 of sgn): x = 2 a + 1.
+__device__ __forceinline__ float awgn_normal_a(const AwgnLds& t, uint32_t a, uint32_t sgn) {
+  const uint32_t x = (a << 1) | 1u;
+  const uint32_t b = __float_as_uint((float)x);
+  const uint32_t i = __builtin_amdgcn_ubfe(b, 18, 14) - 127u * 32u;
+  const float m = fmaf(t.s[i], (float)(b & 0x3ffffu), t.r[i]);
+  return awgn_sign(m, sgn);
 }
 
 // One standard normal from 21 random bits (the low 21 of r).
-__device__ __forceinline__ float awgn_normal(const float2* __restrict__ tab, uint32_t r) {
-  const uint32_t x = ((r & 0xfffffu) << 1) | 1u;
+__device__ __forceinline__ float awgn_normal(const AwgnLds& t, uint32_t r) {
+  const uint32_t x = ((r << 1) & 0x1ffffeu) | 1u;
   const uint32_t b = __float_as_uint((float)x);
-  const float2 rs = tab[(b >> 18) - 127u * 32u];
+  // index (b >> 18) - 127 * 32: the exponent and the top 5 mantissa bits
+  const uint32_t i = __builtin_amdgcn_ubfe(b, 18, 14) - 127u * 32u;
   // S is stored pre-scaled by 2^-18 (exact), so S f = S' (b & 0x3ffff) with the integer converted exactly
-  const float m = fmaf(rs.y, (float)(b & 0x3ffffu), rs.x);
-  return __uint_as_float(__float_as_uint(m) ^ ((r << 11) & 0x80000000u));
+  const float m = fmaf(t.s[i], (float)(b & 0x3ffffu), t.r[i]);
+  return awgn_sign(m, r << 11);
 }
 
 // The tail normal of a component with a = r & 0xfffff < 32 and its 18 extension bits e.
@@ -107,7 +133,7 @@ __device__ __forceinline__ float awgn_tail_normal(uint32_t r, uint32_t e) {
   const uint32_t b = __float_as_uint((float)x);
   const float2 rs = c_awgn_tail[(b >> 18) - 127u * 32u];
   const float m = fmaf(rs.y, (float)(b & 0x3ffffu), rs.x);
-  return __uint_as_float(__float_as_uint(m) ^ ((r << 11) & 0x80000000u));
+  return awgn_sign(m, r << 11);
 }
 
 __device__ __forceinline__ bool awgn_in_tail(uint32_t r) { return (r & 0xfffe0u) == 0u; }
@@ -140,8 +166,8 @@ __device__ __noinline__ float2 awgn_slot_tail(uint64_t seed, uint64_t blk, int s
 }
 
 // The normal pair of slot `slot` (0..2, compile-time after unrolling) of block `blk` (words w).
-__device__ __forceinline__ float2 awgn_slot(const float2* __restrict__ tab, const uint32_t (&w)[4], int slot,
-                                            uint64_t seed, uint64_t blk) {
+__device__ __forceinline__ float2 awgn_slot(const AwgnLds& tab, const uint32_t (&w)[4], int slot, uint64_t seed,
+                                            uint64_t blk) {
   uint32_t r0, r1;
   if (slot == 0) {
     r0 = w[0] >> 11;
@@ -153,7 +179,14 @@ __device__ __forceinline__ float2 awgn_slot(const float2* __restrict__ tab, cons
     r0 = ((w[0] & 0x7ffu) << 10) | ((w[1] & 0x7ffu) >> 1);
     r1 = ((w[2] & 0x7ffu) << 10) | ((w[3] & 0x7ffu) >> 1);
   }
-  const float2 g = make_float2(awgn_normal(tab, r0), awgn_normal(tab, r1));
+  float2 g;
+  if (slot < 2) {  // a = bits 11..30 of the word, the sign its bit 31
+    const uint32_t wa = w[2 * slot], wb = w[2 * slot + 1];
+    g = make_float2(awgn_normal_a(tab, __builtin_amdgcn_ubfe(wa, 11, 20), wa),
+                    awgn_normal_a(tab, __builtin_amdgcn_ubfe(wb, 11, 20), wb));
+  } else {
+    g = make_float2(awgn_normal(tab, r0), awgn_normal(tab, r1));
+  }
   if (__builtin_expect(awgn_in_tail(r0) || awgn_in_tail(r1), 0)) return awgn_slot_tail(seed, blk, slot, r0, r1, g);
   return g;
 }

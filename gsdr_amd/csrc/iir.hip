@@ -213,6 +213,8 @@ struct SetupArgs {
   void* s0;
   double* T;
   int levels;
+  const void* xh;  // the caller's input history, copied to xh_copy for the final pass
+  void* xh_copy;
 };
 
 template <int P>
@@ -245,6 +247,11 @@ struct ScanArgs {
   const double* T0;      // M_0^r, r < 64 (final pass)
   const double* gstart;  // level-1 start states (final pass), or null: s0 is the group start
   const double* s0;
+  // final pass: the caller's history buffers, written by the last chunk (the pass reads the input history
+  // from the tails pass's copy, so no tile reads what the last one overwrites); Pk = K - 1 entries
+  float* xh_out;
+  float* yh_out;
+  int Pk;
 };
 
 // Up-sweep of one level-0 group from the workgroup's tails in LDS (loc = the group's 64 elements),
@@ -308,6 +315,7 @@ __global__ __launch_bounds__(TileShape<S>::WG) void k_iir_chunks(Coeffs cf, cons
     // the extra FIRST workgroup builds the scan constants while the others compute the tails (as the
     // last one it was dispatched after most tiles and finished after them: ~7 us at the kernel's end)
     if (blockIdx.x == 0) {
+      if (setup.xh != nullptr && t < cf.K - 1) static_cast<S*>(setup.xh_copy)[t] = static_cast<const S*>(setup.xh)[t];
       iir_setup<S, P, TSh::WG, kTableInLds<P>>(cf, static_cast<const S*>(setup.yh), static_cast<A*>(setup.s0), setup.T,
                                                setup.levels, reinterpret_cast<double*>(smem));
       return;
@@ -482,12 +490,14 @@ __global__ __launch_bounds__(TileShape<S>::WG) void k_iir_chunks(Coeffs cf, cons
         for (int i = 0; i < P; ++i) tails_d[(c * P + i) * NC + comp] = ys[i];
       } else if constexpr (PASS == kFinal) {
         if (n0 + len == n) {
-          // the last chunk's state after the call (outputs, then inputs, newest first), staged for
-          // the caller's history buffers
+          // the last chunk's state after the call (outputs, then inputs, newest first) into the caller's
+          // history buffers (component comp of entry i)
 #pragma unroll
           for (int i = 0; i < P; ++i) {
-            tails_d[i * NC + comp] = ys[i];
-            tails_d[(P + i) * NC + comp] = (double)(float)xd[i];
+            if (i < sc.Pk) {
+              if (sc.yh_out) sc.yh_out[i * NC + comp] = (float)ys[i];
+              if (sc.xh_out) sc.xh_out[i * NC + comp] = (float)xd[i];
+            }
           }
         }
       }
@@ -747,17 +757,6 @@ __global__ __launch_bounds__(64 * kUpperWaves) void k_iir_scan_upper(uint64_t E1
   }
 }
 
-// The caller's history buffers after the call, from the state staged by the last chunk.
-template <class S>
-__global__ __launch_bounds__(64) void k_iir_history(S* __restrict__ xh, S* __restrict__ yh,
-                                                    const typename Acc<S>::type* __restrict__ st, int P, int Pk) {
-  const int i = threadIdx.x;
-  if (i < Pk) {
-    if (yh) yh[i] = to_sample(st[i]);
-    if (xh) xh[i] = to_sample(st[P + i]);
-  }
-}
-
 template <class S, int P>
 static hipError_t run(const Coeffs& cf, S* xh, S* yh, const S* x, S* y, uint64_t n, hipStream_t st) {
   using A = typename Acc<S>::type;
@@ -790,8 +789,8 @@ static hipError_t run(const Coeffs& cf, S* xh, S* yh, const S* x, S* y, uint64_t
   bytes += (size_t)(levels + 1) * kGroup * P * P * sizeof(double);  // T[level][r] = M_level^r
   const size_t off_s0 = bytes;
   bytes += P * sizeof(A);
-  const size_t off_st = bytes;  // exit state staged by the last chunk: P outputs, then P inputs
-  bytes += 2 * P * sizeof(A);
+  const size_t off_xh = bytes;  // the caller's input history, copied by the tails pass for the final pass
+  bytes += (P * sizeof(S) + 15) / 16 * 16;
   char* ws = nullptr;
   hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&ws), bytes, st);
   if (e != hipSuccess) return e;
@@ -799,7 +798,7 @@ static hipError_t run(const Coeffs& cf, S* xh, S* yh, const S* x, S* y, uint64_t
   auto starts = [&](int k) { return reinterpret_cast<A*>(ws + off[k][1]); };
   auto table = [&](int k) { return reinterpret_cast<double*>(ws + off_m) + (size_t)k * kGroup * P * P; };
   A* s0 = reinterpret_cast<A*>(ws + off_s0);
-  A* st_out = reinterpret_cast<A*>(ws + off_st);
+  S* xh_copy = reinterpret_cast<S*>(ws + off_xh);
   const int K = cf.K;
   const int Pk = K - 1;  // live state components (<= P); the rest stay zero
 
@@ -807,12 +806,12 @@ static hipError_t run(const Coeffs& cf, S* xh, S* yh, const S* x, S* y, uint64_t
   const uint64_t ntiles = ceil_div<uint64_t>(n, TileShape<S>::TS);
   if (ntiles >= 0x7fffffffull) return hipErrorInvalidValue;  // one workgroup per tile (k_iir_chunks)
   const uint32_t blocks = (uint32_t)ntiles;
-  const SetupArgs sa{yh, s0, table(0), levels};
+  const SetupArgs sa{yh, s0, table(0), levels, xh, xh_copy};
   const bool vec = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15u) == 0;
   // fused: the tails pass leaves level-0 inclusive prefixes in starts(0) and the group aggregates in
   // elems(1); the final pass finishes level 0 itself
   const ScanArgs up_args{reinterpret_cast<double*>(starts(0)), levels > 0 ? reinterpret_cast<double*>(elems(1)) : nullptr,
-                         nullptr, nullptr, nullptr};
+                         nullptr, nullptr, nullptr, nullptr, nullptr, 0};
   if (vec) {
     k_iir_chunks<S, P, kTails, true, F><<<blocks + 1, WG, 0, st>>>(cf, x, xh, n, nullptr, elems(0), nullptr, sa, up_args);
   } else {
@@ -850,17 +849,20 @@ static hipError_t run(const Coeffs& cf, S* xh, S* yh, const S* x, S* y, uint64_t
     k_iir_down<A, P><<<(uint32_t)ceil_div<uint64_t>(E[k], kGroup), 64, 0, st>>>(E[k], table(k), starts(k + 1),
                                                                                starts(k));
   }
+  // the last chunk writes the caller's history itself (round 4: one launch fewer than a separate history
+  // kernel); the input history it reads comes from the tails pass's copy
   const ScanArgs down_args{reinterpret_cast<double*>(starts(0)), nullptr, table(0),
                            levels > 0 ? reinterpret_cast<const double*>(starts(1)) : nullptr,
-                           reinterpret_cast<const double*>(s0)};
+                           reinterpret_cast<const double*>(s0), reinterpret_cast<float*>(xh),
+                           reinterpret_cast<float*>(yh), Pk};
+  const S* xh_in = xh ? xh_copy : nullptr;
   if (vec) {
-    k_iir_chunks<S, P, kFinal, true, F><<<blocks, WG, 0, st>>>(cf, x, xh, n, starts(0), st_out, y, SetupArgs{},
+    k_iir_chunks<S, P, kFinal, true, F><<<blocks, WG, 0, st>>>(cf, x, xh_in, n, starts(0), nullptr, y, SetupArgs{},
                                                                down_args);
   } else {
-    k_iir_chunks<S, P, kFinal, false, F><<<blocks, WG, 0, st>>>(cf, x, xh, n, starts(0), st_out, y, SetupArgs{},
+    k_iir_chunks<S, P, kFinal, false, F><<<blocks, WG, 0, st>>>(cf, x, xh_in, n, starts(0), nullptr, y, SetupArgs{},
                                                                 down_args);
   }
-  if (xh || yh) k_iir_history<S><<<1, 64, 0, st>>>(xh, yh, st_out, P, Pk);
   e = launch_status();
   const hipError_t f = hipFreeAsync(ws, st);
   return e != hipSuccess ? e : f;

@@ -153,28 +153,54 @@ __device__ __noinline__ uint32_t demod_rect_tie(float dx0, float dx1, float dx2,
   return idx;
 }
 
+typedef float gsdr_f32x2 __attribute__((ext_vector_type(2)));
+
+// floor(v + 0.5) as an integer in one instruction (v_cvt_rpi_i32_f32); the centre of the 3 x 3 neighbourhood.
+// (It differs from rintf only at exact halves, where both nearest levels are in either neighbourhood.)
+__device__ __forceinline__ int cvt_rpi(float v) {
+  int r;
+  asm("v_cvt_rpi_i32_f32 %0, %1" : "=v"(r) : "v"(v));
+  return r;
+}
+
+// The three per-axis candidates (levels c - 1, c, c + 1 of the padded array lp): squared differences e0..e2
+// (the first two on packed instructions, straight from the two loaded levels), their minimum, median and
+// the first index reaching the minimum.
+struct AxisCand {
+  float d[3], e[3], emin, emed;
+  int arg;
+};
+__device__ __forceinline__ AxisCand axis_cand(const float* __restrict__ lp, float v) {
+  AxisCand c;
+  const gsdr_f32x2 l01 = gsdr_f32x2{lp[0], lp[1]};
+  const gsdr_f32x2 d01 = gsdr_f32x2{v, v} - l01;  // __fsub_rn each: -ffp-contract=off, no fusing
+  const float d2 = v - lp[2];
+  const gsdr_f32x2 e01 = d01 * d01;
+  c.d[0] = d01.x;
+  c.d[1] = d01.y;
+  c.d[2] = d2;
+  c.e[0] = e01.x;
+  c.e[1] = e01.y;
+  c.e[2] = d2 * d2;
+  c.emin = fminf(fminf(c.e[0], c.e[1]), c.e[2]);
+  c.emed = __builtin_amdgcn_fmed3f(c.e[0], c.e[1], c.e[2]);
+  c.arg = c.e[0] == c.emin ? 0 : (c.e[1] == c.emin ? 1 : 2);
+  return c;
+}
+
 __device__ __forceinline__ uint32_t demod_rect_fast(const float* __restrict__ lxp, const float* __restrict__ lyp, float2 r,
                                                     float lim, float scale) {
   if (!(fabsf(r.x) <= lim && fabsf(r.y) <= lim)) return 256u;
-  const int i0 = nearest_level(r.x, scale);
-  const int q0 = nearest_level(r.y, scale);
-  float dx[3], dy[3], ex[3], ey[3];
-#pragma unroll
-  for (int d = 0; d < 3; ++d) {
-    dx[d] = __fsub_rn(r.x, lxp[i0 + d]);
-    dy[d] = __fsub_rn(r.y, lyp[q0 + d]);
-    ex[d] = __fmul_rn(dx[d], dx[d]);
-    ey[d] = __fmul_rn(dy[d], dy[d]);
+  // level i sits at (i - 7.5) / 7.5 * a  =>  i ~= v * (7.5 / a) + 7.5 (both axes in one packed fma)
+  const gsdr_f32x2 u = __builtin_elementwise_fma(gsdr_f32x2{r.x, r.y}, gsdr_f32x2{scale, scale}, gsdr_f32x2{7.5f, 7.5f});
+  const int i0 = min(max(cvt_rpi(u.x), 0), 15);
+  const int q0 = min(max(cvt_rpi(u.y), 0), 15);
+  const AxisCand cx = axis_cand(lxp + i0, r.x), cy = axis_cand(lyp + q0, r.y);
+  const float thr = tie_threshold(__fadd_rn(cx.emin, cy.emin));
+  if (__fadd_rn(cx.emed, cy.emin) > thr && __fadd_rn(cx.emin, cy.emed) > thr) {
+    return (uint32_t)((i0 - 1 + cx.arg) * 16 + (q0 - 1 + cy.arg));
   }
-  const float exm = fminf(fminf(ex[0], ex[1]), ex[2]);
-  const float eym = fminf(fminf(ey[0], ey[1]), ey[2]);
-  const float ex2 = __builtin_amdgcn_fmed3f(ex[0], ex[1], ex[2]);
-  const float ey2 = __builtin_amdgcn_fmed3f(ey[0], ey[1], ey[2]);
-  const int a = ex[0] == exm ? 0 : (ex[1] == exm ? 1 : 2);
-  const int b = ey[0] == eym ? 0 : (ey[1] == eym ? 1 : 2);
-  const float thr = tie_threshold(__fadd_rn(exm, eym));
-  if (__fadd_rn(ex2, eym) > thr && __fadd_rn(exm, ey2) > thr) return (uint32_t)((i0 - 1 + a) * 16 + (q0 - 1 + b));
-  return demod_rect_tie(dx[0], dx[1], dx[2], dy[0], dy[1], dy[2], i0, q0);
+  return demod_rect_tie(cx.d[0], cx.d[1], cx.d[2], cy.d[0], cy.d[1], cy.d[2], i0, q0);
 }
 
 __device__ __forceinline__ void load_table(float2* lds_tab, uint32_t type) {
@@ -254,7 +280,7 @@ __global__ __launch_bounds__(kCBlock) void k_c256_mod_awgn(const uint8_t* __rest
                                                             uint32_t n, uint32_t type, float sigma, uint64_t seed,
                                                             uint64_t first) {
   __shared__ float2 tab[256];
-  __shared__ float2 ntab[kAwgnTableSize];
+  __shared__ AwgnLds ntab;
   __shared__ float4 stage[kCBlock / 64][kAwgnWaveSyms / 2];  // per wave: 384 symbols as 192 float4
   awgn_load_table(ntab, kCBlock);
   load_table(tab, type);  // its barrier publishes both tables
@@ -320,8 +346,12 @@ __global__ __launch_bounds__(kCBlock) void k_c256_mod_awgn(const uint8_t* __rest
 // Both fall back to the exhaustive search for inputs their fast path does not cover.
 template <int TYPE>
 __global__ __launch_bounds__(kCBlock) void k_c256_demod(C256Streams st, uint32_t n) {
-  __shared__ float2 tab[256];
-  __shared__ float lxp[18], lyp[18];  // rectangular levels, padded with +inf (demod_rect_fast)
+  // the rectangular levels, padded with +inf (demod_rect_fast), at the start of the table's LDS block: their
+  // reads then need no base add (ds_read2_b32 offsets reach 1 KB)
+  __shared__ float2 tab_lev[20 + 256];
+  float* const lxp = reinterpret_cast<float*>(tab_lev);
+  float* const lyp = lxp + 20;
+  float2* const tab = tab_lev + 20;
   // the circular cell lists: an LDS image of g_circ_cells (cell words and the distinct lists)
   __shared__ uint4 ccells[TYPE == 0 ? 1 : sizeof(CircCells) / 16];
   const uint16_t* cword = reinterpret_cast<const CircCells*>(ccells)->cell;

@@ -40,6 +40,9 @@ def timed(name, fn):
 
 
 timed("fm_chain_int8", lambda: ops.fm_demod(x8, taps, 1e6, 0.0, 1e5, 2e4, D, 0, n_fm, out=out))
+timed("am_chain_int8", lambda: ops.am_demod(x8, taps, 1e6, 0.0, 1e5, D, 0, n_fm, out=out))
+yc = torch.empty(n_fm + 1, dtype=torch.complex64, device=dev)
+timed("fir_int8", lambda: ops.fir(taps, x8, D, n_fm + 1, out=yc))
 timed("qpsk256_mod_awgn", lambda: ops.qpsk256_modulate_awgn(syms, 0, 0.02, 0x5EED0005, 0, out=rx))
 timed("qpsk256_demod_rect", lambda: ops.qpsk256_demodulate(rx, 0, out=dec))
 timed("qpsk256_mod", lambda: ops.qpsk256_modulate(syms, 0, 1.0, out=rx))

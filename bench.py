@@ -417,6 +417,15 @@ def secondary_configs(torch, ops, device, taps):
             "channel_msamples_per_s": round(C * n_in / t / 1e6, 1),
             "speedup_vs_single_calls": round(C * out["fm_chain"]["us_per_launch"] / (t * 1e6), 2)}
         del ym
+    # streaming object on complex float input: one launch per call (round 4), C equal
+    # chunks per 64 M-sample channel pass, against one call
+    out["fir_stream"] = stream_rate(torch, abi, device, taps, xs, stream, out_fir_call(torch, abi, device, taps, xs,
+                                                                                      stream),
+                                    kind=0, fmt=0, chunk_counts=(1, 8, 32), label="config 2's complex float channel "
+                                    "through gsdrxStream (CF32 FIR, D = 4), C chunks a pass")
+    out["fm_stream"] = stream_rate(torch, abi, device, taps, xs, stream, out["fm_chain"]["us_per_launch"] * 1e-6,
+                                   kind=1, fmt=0, chunk_counts=(1, 8, 32), label="config 3's channel through "
+                                   "gsdrxStream (CF32 FM chain, D = 4), C chunks a pass")
     del xs
     # int8 I/Q front end fused into the filter: 2 instead of 8 input bytes per sample; the FM chain gets
     # config 3's signal quantised to int8 (x 100), consecutive batches of one channel
@@ -447,7 +456,9 @@ def secondary_configs(torch, ops, device, taps):
                        "us_per_launch": round(t * 1e6, 2), "msamples_per_s": round(N_IN / t / 1e6, 1),
                        "alg_gbps": round(b / t / 1e9, 1), "alg_bytes_per_launch": b,
                        "fma_tflops": round(4 * TAPS * N_OUT / t / 1e12, 1)}
-    out["fir_int8_stream"] = int8_stream_rate(torch, abi, device, taps, x8s, stream, t)
+    out["fir_int8_stream"] = stream_rate(torch, abi, device, taps, x8s, stream, t, kind=0, fmt=1, chunk_counts=(1, 2, 8),
+                                         label="config 2's int8 I/Q channel through gsdrxStream (CS8 FIR, D = 4), C "
+                                         "chunks a pass")
     del x8s, yf
     # true recursive IIR: 4th-order Butterworth over 2^24 samples
     from scipy import signal as sps
@@ -548,32 +559,40 @@ def secondary_configs(torch, ops, device, taps):
     return out, c5
 
 
-def int8_stream_rate(torch, abi, device, taps, x8s, stream, t_call, chunk_counts=(1, 2, 8)):
-    """SURVEY.md 8(f) rows 1 + 2: config 2's int8 channel fed through a gsdrxStream (CS8 FIR, D = 4) in
-    C equal chunks per pass, passes rotating over the batches, against one gsdrxFirFCInt8 call (t_call).
-    At decimation 4 every gsdrxStreamProcess call is ONE launch of the same matrix-core kernel (seam
-    samples from the history buffer, next history written by the launch), so the difference is the
-    per-launch fixed cost (~6.5 us: launch, tap split, first tile's load latency) times C, and the host's
-    issue time per call (host_us_per_call, measured over the same loop)."""
+def out_fir_call(torch, abi, device, taps, xs, stream):
+    """One gsdrFirFC call over a whole 64 M-sample channel (the stream lines' reference)."""
+    y = torch.empty(N_OUT, dtype=torch.complex64, device=device)
+    argsets = [(DECIM, taps.data_ptr(), TAPS, x.data_ptr(), y.data_ptr(), N_OUT, device.index, stream) for x in xs]
+    return time_abi(torch, abi.lib.gsdrFirFC, argsets)
+
+
+def stream_rate(torch, abi, device, taps, xs, stream, t_call, kind, fmt, chunk_counts, label):
+    """SURVEY.md 8(f) row 1 (and row 2 for int8 I/Q): a 64 M-sample channel fed through a gsdrxStream in C
+    equal chunks per pass, passes rotating over the batches, against one call of the entry point (t_call).
+    Every gsdrxStreamProcess call is ONE launch of the kernel one monolithic call runs (seam samples from
+    the history buffer, next history written by the launch: the int8 matrix-core kernels since round 3,
+    the float tiled kernels since round 4), so the difference is the per-launch fixed cost times C and the
+    host's issue time per call (host_us_per_call, measured over the same loop)."""
     import ctypes
 
-    res = {"config": "config 2's int8 I/Q channel through gsdrxStream (CS8 FIR, D = 4), C chunks a pass",
-           "single_call_us": round(t_call * 1e6, 2)}
+    res = {"config": label, "single_call_us": round(t_call * 1e6, 2)}
+    sb = 2 if fmt == 1 else 8
     y = torch.empty(N_OUT + 1024, dtype=torch.complex64, device=device)  # a call can emit the history's outputs too
     yp, ycap = y.data_ptr(), y.numel()
     written = ctypes.c_size_t()
     wref = ctypes.byref(written)
+    f = ctypes.c_float
     for chunks in chunk_counts:
         h = ctypes.c_void_p()
-        rc = abi.lib.gsdrxStreamCreate(ctypes.byref(h), 0, 1, DECIM, taps.data_ptr(), TAPS, 1.0, 0.0, 0.0, 1.0, 0,
-                                       device.index)
+        rc = abi.lib.gsdrxStreamCreate(ctypes.byref(h), kind, fmt, DECIM, taps.data_ptr(), TAPS, f(1.0e6), f(0.0),
+                                       f(1.0e5), f(2.0e4), 0, device.index)
         assert rc == 0, rc
         cs = N_IN // chunks
         argsets = []
-        for x in x8s:
+        for x in xs:
             for c in range(chunks):
                 n = cs if c < chunks - 1 else N_IN - cs * (chunks - 1)
-                argsets.append((h, x.data_ptr() + 2 * cs * c, n, yp, ycap, wref, stream))
+                argsets.append((h, x.data_ptr() + sb * cs * c, n, yp, ycap, wref, stream))
         fn = abi.lib.gsdrxStreamProcess
         k = 0
         for _ in range(max(20, 8 * chunks)):

@@ -476,18 +476,20 @@ hipError_t launch_poly_default(const FirJob& j, hipStream_t s) {
 
 // Decimation 4 (the headline shape, complex or int8 I/Q samples) with the tile sized to the call: the
 // 1,024-output tiles (WG 256, R 4) measured fastest for a whole channel, but a short call (a stream chunk)
-// of fewer tiles than two rounds of workgroup slots is one tile's latency on part of the chip; 512- and
-// 256-output tiles (WG 128 / 64, same R and JC) put more of the chip on it. The per-output MAC order
-// depends only on (D, JC), so every tile size gives the same outputs bit for bit.
+// of fewer tiles than two rounds of workgroup slots is one wave's latency on part of the chip (kernel
+// trace: 512 workgroups of 64 threads took 7.2 us for 131 K outputs). Short calls take 256-thread
+// workgroups with fewer outputs a thread (R = 2 or 1): more waves on the call, each with a shorter
+// multiply-add chain. The per-output MAC order depends only on (D, JC), so every tile shape gives the
+// same outputs bit for bit.
 template <class TapT, class InT, int MODE>
 hipError_t launch_poly_d4(const FirJob& j, hipStream_t s) {
   int cus = 0;
   if (current_device_cus(&cus) == hipSuccess && cus > 0) {
     const uint64_t slots = (uint64_t)cus * 4;  // 38 KB tiles: 4 workgroups a CU
-    const uint64_t t256 = ceil_div<uint64_t>(j.N, 1024);
-    if (t256 < 2 * slots) {
-      if (ceil_div<uint64_t>(j.N, 512) >= 2 * slots) return launch_poly<TapT, InT, 4, 4, 16, 128, MODE, 0, true>(j, s);
-      return launch_poly<TapT, InT, 4, 4, 16, 64, MODE, 0, true>(j, s);
+    const uint64_t t1024 = ceil_div<uint64_t>(j.N, 1024);
+    if (t1024 < 2 * slots) {
+      if (ceil_div<uint64_t>(j.N, 512) >= 2 * slots) return launch_poly<TapT, InT, 4, 2, 16, 256, MODE, 0, true>(j, s);
+      return launch_poly<TapT, InT, 4, 1, 16, 256, MODE, 0, true>(j, s);
     }
   }
   return launch_poly_default<TapT, InT, 4, 4, 16, 256, MODE>(j, s);

@@ -47,3 +47,20 @@ timed("qpsk256_mod_awgn", lambda: ops.qpsk256_modulate_awgn(syms, 0, 0.02, 0x5EE
 timed("qpsk256_demod_rect", lambda: ops.qpsk256_demodulate(rx, 0, out=dec))
 timed("qpsk256_mod", lambda: ops.qpsk256_modulate(syms, 0, 1.0, out=rx))
 timed("fm_chain", lambda: ops.fm_demod(xf, taps, 1e6, 0.0, 1e5, 2e4, D, 0, n_fm, out=out))
+
+# IIR (4th-order Butterworth, 2^24 samples) as bench.py times it (no history buffers) and with history
+from scipy import signal as sps  # noqa: E402
+
+from gsdr_amd import abi  # noqa: E402
+
+stream = torch.cuda.current_stream(dev).cuda_stream
+bb, aa = (torch.tensor(v, dtype=torch.float32, device=dev) for v in sps.butter(4, 0.1))
+for dt, name in ((torch.float32, "gsdrIirFF"), (torch.complex64, "gsdrIirCC")):
+    xi = torch.rand(1 << 24, dtype=dt, device=dev, generator=g)
+    yi = torch.empty_like(xi)
+    hx = torch.zeros(4, dtype=dt, device=dev)
+    hy = torch.zeros(4, dtype=dt, device=dev)
+    fn = getattr(abi.lib, name)
+    timed(name, lambda: fn(bb.data_ptr(), aa.data_ptr(), 5, None, None, xi.data_ptr(), yi.data_ptr(), 1 << 24, 0, stream))
+    timed(name + "+history", lambda: fn(bb.data_ptr(), aa.data_ptr(), 5, hx.data_ptr(), hy.data_ptr(), xi.data_ptr(),
+                                        yi.data_ptr(), 1 << 24, 0, stream))

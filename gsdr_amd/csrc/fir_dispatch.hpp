@@ -210,7 +210,7 @@ hipError_t launch_contig(const FirJob& j, hipStream_t s) {
 //   7 generic kernel | 8 default shape with plain (temporal) loads/stores | 9 default, XCD-aware tile order
 //   10/11 default, tile stored through LDS | 13 matrix-core core (k_fir_mfma_bc, T <= 132)
 //   14 default, tile body staged by LDS-DMA (global_load_lds)
-//   24 WG=64 R=4 | 28 WG=128 R=4
+//   24 WG=64 R=4 | 25 WG=256 R=2 | 26 WG=256 R=1 | 28 WG=128 R=4
 // Ablation probes (fir.hip, compiled only into the probes library, `make probes`; the product library
 // returns hipErrorInvalidValue for them): 104 compute only, 105 staging only, 107 staging only
 // (non-temporal), 113 matrix-core compute only, 117 staging only by LDS-DMA, 110/111 streaming ceiling
@@ -250,6 +250,10 @@ hipError_t launch_d4_complex(const FirJob& j, hipStream_t s) {
       return launch_poly<TapT, InT, 4, 4, 16, 256, MODE, 0, true, false, 0, true>(j, s);
     case 24:
       return launch_poly<TapT, InT, 4, 4, 16, 64, MODE, 0, true>(j, s);
+    case 25:  // WG 256, R 2 (512-output tiles; a short-call shape)
+      return launch_poly<TapT, InT, 4, 2, 16, 256, MODE, 0, true>(j, s);
+    case 26:  // WG 256, R 1 (256-output tiles)
+      return launch_poly<TapT, InT, 4, 1, 16, 256, MODE, 0, true>(j, s);
     case 28:
       return launch_poly<TapT, InT, 4, 4, 16, 128, MODE, 0, true>(j, s);
     default:
@@ -475,22 +479,19 @@ hipError_t launch_poly_default(const FirJob& j, hipStream_t s) {
 }
 
 // Decimation 4 (the headline shape, complex or int8 I/Q samples) with the tile sized to the call: the
-// 1,024-output tiles (WG 256, R 4) measured fastest for a whole channel, but a short call (a stream chunk)
-// of fewer tiles than two rounds of workgroup slots is one wave's latency on part of the chip (kernel
-// trace: 512 workgroups of 64 threads took 7.2 us for 131 K outputs). Short calls take 256-thread
-// workgroups with fewer outputs a thread (R = 2 or 1): more waves on the call, each with a shorter
-// multiply-add chain. The per-output MAC order depends only on (D, JC), so every tile shape gives the
-// same outputs bit for bit.
+// 1,024-output tiles (WG 256, R 4) measured fastest for a whole channel, but a call of a few rounds of
+// workgroup slots (a stream chunk) pays each round's latency on part of the chip. Kernel trace of the shapes
+// (tools/short_call_shapes.py, profiles/r04_short_call_shapes.txt): at 2.1 M / 524 K / 131 K outputs
+// WG 256 R 4 took 24.5 / 9.0 / 6.3 us, WG 256 R 2 (512-output tiles) 22.0 / 8.5 / 5.4, WG 64 R 4
+// 23.5 / 8.9 / 5.7, WG 256 R 1 29.2 / 9.9 / 5.1 -- so calls of fewer than three rounds of 1,024-output
+// tiles take R 2. The per-output MAC order depends only on (D, JC): every shape gives the same outputs bit
+// for bit.
 template <class TapT, class InT, int MODE>
 hipError_t launch_poly_d4(const FirJob& j, hipStream_t s) {
   int cus = 0;
   if (current_device_cus(&cus) == hipSuccess && cus > 0) {
     const uint64_t slots = (uint64_t)cus * 4;  // 38 KB tiles: 4 workgroups a CU
-    const uint64_t t1024 = ceil_div<uint64_t>(j.N, 1024);
-    if (t1024 < 2 * slots) {
-      if (ceil_div<uint64_t>(j.N, 512) >= 2 * slots) return launch_poly<TapT, InT, 4, 2, 16, 256, MODE, 0, true>(j, s);
-      return launch_poly<TapT, InT, 4, 1, 16, 256, MODE, 0, true>(j, s);
-    }
+    if (ceil_div<uint64_t>(j.N, 1024) < 3 * slots) return launch_poly<TapT, InT, 4, 2, 16, 256, MODE, 0, true>(j, s);
   }
   return launch_poly_default<TapT, InT, 4, 4, 16, 256, MODE>(j, s);
 }

@@ -1309,21 +1309,42 @@ struct LdsPair<float2> {
 
 // N separate ds_read_b64 of the 8-byte values at p[0..N): the compiler merges adjacent 8-byte LDS loads
 // into ds_read2_b64, which takes 16 LDS cycles per 16 bytes against 4 for two ds_read_b64 (and banks
-// mod 32), so at odd D the one-sample-a-read loop ran at a quarter of the LDS rate. Issued as inline
-// asm, waited for together (lgkmcnt(0) covers the reads; each result is then tied to that wait).
+// mod 32), so at odd D the one-sample-a-read loop ran at a quarter of the LDS rate. The reads and their
+// wait are ONE asm statement with early-clobber outputs, so no register is taken as written before the
+// s_waitcnt that fills it (a copy scheduled between separate read and wait statements would
+// have read a register the load had not filled yet).
+#define GSDR_R8(i) "ds_read_b64 %" #i ", %[a] offset:" #i "*8\n\t"
 template <int N>
-__device__ __forceinline__ void lds_read_b64_n(const float2* p, float2 (&out)[N]) {
+__device__ __forceinline__ void lds_read_b64_n(const float2* p, float2 (&out)[N]);
+template <>
+__device__ __forceinline__ void lds_read_b64_n<8>(const float2* p, float2 (&out)[8]) {
   const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float2*)p;
-  gsdr_f32x2 r[N];
+  gsdr_f32x2 r0, r1, r2, r3, r4, r5, r6, r7;
+  asm volatile(GSDR_R8(0) GSDR_R8(1) GSDR_R8(2) GSDR_R8(3) GSDR_R8(4) GSDR_R8(5) GSDR_R8(6) GSDR_R8(7)
+               "s_waitcnt lgkmcnt(0)"
+               : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3), "=&v"(r4), "=&v"(r5), "=&v"(r6), "=&v"(r7)
+               : [a] "v"(a)
+               : "memory");
+  const gsdr_f32x2 r[8] = {r0, r1, r2, r3, r4, r5, r6, r7};
 #pragma unroll
-  for (int i = 0; i < N; ++i) asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(r[i]) : "v"(a), "i"(8 * i) : "memory");
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    asm volatile("" : "+v"(r[i]));
-    out[i] = make_float2(r[i].x, r[i].y);
-  }
+  for (int i = 0; i < 8; ++i) out[i] = make_float2(r[i].x, r[i].y);
 }
+template <>
+__device__ __forceinline__ void lds_read_b64_n<16>(const float2* p, float2 (&out)[16]) {
+  const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float2*)p;
+  gsdr_f32x2 r0, r1, r2, r3, r4, r5, r6, r7, r8, r9, r10, r11, r12, r13, r14, r15;
+  asm volatile(GSDR_R8(0) GSDR_R8(1) GSDR_R8(2) GSDR_R8(3) GSDR_R8(4) GSDR_R8(5) GSDR_R8(6) GSDR_R8(7)
+               GSDR_R8(8) GSDR_R8(9) GSDR_R8(10) GSDR_R8(11) GSDR_R8(12) GSDR_R8(13) GSDR_R8(14) GSDR_R8(15)
+               "s_waitcnt lgkmcnt(0)"
+               : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3), "=&v"(r4), "=&v"(r5), "=&v"(r6), "=&v"(r7),
+                 "=&v"(r8), "=&v"(r9), "=&v"(r10), "=&v"(r11), "=&v"(r12), "=&v"(r13), "=&v"(r14), "=&v"(r15)
+               : [a] "v"(a)
+               : "memory");
+  const gsdr_f32x2 r[16] = {r0, r1, r2, r3, r4, r5, r6, r7, r8, r9, r10, r11, r12, r13, r14, r15};
+#pragma unroll
+  for (int i = 0; i < 16; ++i) out[i] = make_float2(r[i].x, r[i].y);
+}
+#undef GSDR_R8
 
 template <class TapT, class InT, int IC, int WG, bool VEC, int MODE, bool PAIR = false>
 __global__ __launch_bounds__(WG) void k_fir_rt(FirParams p) {

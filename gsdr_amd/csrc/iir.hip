@@ -673,98 +673,45 @@ __device__ __forceinline__ void mat_vec_acc(const double* __restrict__ M, const 
   }
 }
 
-// T[k] = M_k^r, r < 64 (setup tables); elems1 = level-1 elements (the tails pass's level-0 group aggregates),
-// starts1 = their start states (written here). Round 4: level 1's up-sweep is folded in (one launch fewer):
-//   a. every workgroup forms all E2 level-2 elements (the level-1 group aggregates, agg_g = sum_r M_1^(last-r)
-//      e_(64 g + r): one matrix-vector product a lane with its own power M_1^(last - r), then a lane sum),
-//      its 16 waves taking the groups in turn, into LDS;
-//   b. waves 0..3 run the Hillis-Steele up-sweep of their own level-1 group (its inclusive prefixes);
-//   c. as before: level 2 scanned from LDS, the level-2 start states, level 1's down-sweep.
-// 16 waves share the aggregates for P <= 4 (two register sets of P x P doubles a lane fit 128 VGPRs); larger
-// states keep round 3's 4 waves (512 VGPRs a lane)
+// T[k] = M_k^r, r < 64 (setup tables); elems1 = level-1 elements (their inclusive prefixes in starts1 from
+// k_iir_up, overwritten with start states), elems2 = level-2 elements (group aggregates of level 1)
 template <int P>
-constexpr int kUpperAggWaves = P <= 4 ? 16 : kUpperWaves;
-template <int P>
-__global__ __launch_bounds__(64 * kUpperAggWaves<P>) void k_iir_scan_upper(uint64_t E1, uint64_t E2, int NC,
-                                                                        const double* __restrict__ T1,
-                                                                        const double* __restrict__ T2,
-                                                                        const double* __restrict__ T3,
-                                                                        const double* __restrict__ elems1,
-                                                                        const double* __restrict__ s0,
-                                                                        double* __restrict__ starts1) {
+__global__ __launch_bounds__(64 * kUpperWaves) void k_iir_scan_upper(uint64_t E1, uint64_t E2, int NC,
+                                                                     const double* __restrict__ T1,
+                                                                     const double* __restrict__ T2,
+                                                                     const double* __restrict__ T3,
+                                                                     const double* __restrict__ elems2,
+                                                                     const double* __restrict__ s0,
+                                                                     double* __restrict__ starts1) {
   constexpr int PP = P * P;
-  __shared__ double aggs2[kUpperE2][P];      // level-2 elements (level-1 group aggregates)
   __shared__ double incl2[kUpperE2][P];      // level-2 zero-state inclusive prefixes within their group
   __shared__ double gstart[kUpperWaves][P];  // level-2 group start states
   const int comp = blockIdx.y;
   const int t = threadIdx.x, r = t % 64, w = t / 64;
-  // a. the level-1 group aggregates (full groups: lane r weighs its element by M_1^(63 - r))
-  {
-    const uint64_t ngroups = E2;
-    double mr[PP];
-#pragma unroll
-    for (int q = 0; q < PP; ++q) mr[q] = T1[(size_t)(63 - r) * PP + q];
-    for (uint64_t g = (uint64_t)w; g < ngroups; g += kUpperAggWaves<P>) {
-      const uint64_t j = g * kGroup + r;
-      const uint64_t last = (E1 - 1 < g * kGroup + kGroup - 1) ? E1 - 1 - g * kGroup : kGroup - 1;
-      double e[P], acc[P];
-#pragma unroll
-      for (int i = 0; i < P; ++i) {
-        e[i] = j < E1 ? elems1[(j * P + i) * NC + comp] : 0.0;
-        acc[i] = 0.0;
-      }
-      if (last == kGroup - 1) {
-        mat_vec_acc<P>(mr, e, acc);
-      } else if ((uint64_t)r <= last) {  // the partial last group: M_1^(last - r)
-        mat_vec_acc<P>(T1 + (size_t)(last - r) * PP, e, acc);
-      }
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-#pragma unroll
-        for (int i = 0; i < P; ++i) acc[i] += __shfl_xor(acc[i], o, 64);
-      }
-      if (r < P) aggs2[g][r] = acc[r];
-    }
-  }
-  // this wave's level-1 group (= level-2 element) and its operands
+  // this wave's level-1 group (= level-2 element) and its own operands, loaded first
   const uint64_t e2 = (uint64_t)blockIdx.x * kUpperWaves + w;
   const uint64_t e1 = e2 * kGroup + r;
-  const bool own = w < kUpperWaves;
-  const bool live = own && e2 < E2 && e1 < E1;
+  const bool live = e2 < E2 && e1 < E1;
   double mine[P], m1r[PP];
-  if (own) {
-    // b. the inclusive zero-state prefixes of this level-1 group (k_iir_up's Hillis-Steele, same operations)
 #pragma unroll
-    for (int i = 0; i < P; ++i) mine[i] = live ? elems1[(e1 * P + i) * NC + comp] : 0.0;
+  for (int i = 0; i < P; ++i) mine[i] = live ? starts1[(e1 * P + i) * NC + comp] : 0.0;
 #pragma unroll
-    for (int s = 0; s < 6; ++s) {
-      const int d = 1 << s;
-      double u[P];
+  for (int q = 0; q < PP; ++q) m1r[q] = T1[(size_t)r * PP + q];
+  // 1. level 2: every workgroup scans all E2 elements, wave j the group j (one element a lane)
+  double v[P];
+  const uint64_t j2 = (uint64_t)t;
 #pragma unroll
-      for (int i = 0; i < P; ++i) u[i] = __shfl_up(mine[i], d, 64);
-      if (r >= d) mat_vec_acc<P>(T1 + (size_t)d * PP, u, mine);
-    }
+  for (int i = 0; i < P; ++i) v[i] = j2 < E2 ? elems2[(j2 * P + i) * NC + comp] : 0.0;
 #pragma unroll
-    for (int q = 0; q < PP; ++q) m1r[q] = T1[(size_t)r * PP + q];
+  for (int s = 0; s < 6; ++s) {
+    const int d = 1 << s;
+    double u[P];
+#pragma unroll
+    for (int i = 0; i < P; ++i) u[i] = __shfl_up(v[i], d, 64);
+    if (r >= d) mat_vec_acc<P>(T2 + (size_t)d * PP, u, v);
   }
-  __syncthreads();
-  // 1. level 2: every workgroup scans all E2 elements, wave j < 4 the group j (one element a lane)
-  if (own) {
-    double v[P];
-    const uint64_t j2 = (uint64_t)t;
 #pragma unroll
-    for (int i = 0; i < P; ++i) v[i] = j2 < E2 ? aggs2[j2][i] : 0.0;
-#pragma unroll
-    for (int s = 0; s < 6; ++s) {
-      const int d = 1 << s;
-      double u[P];
-#pragma unroll
-      for (int i = 0; i < P; ++i) u[i] = __shfl_up(v[i], d, 64);
-      if (r >= d) mat_vec_acc<P>(T2 + (size_t)d * PP, u, v);
-    }
-#pragma unroll
-    for (int i = 0; i < P; ++i) incl2[t][i] = v[i];
-  }
+  for (int i = 0; i < P; ++i) incl2[t][i] = v[i];
   __syncthreads();
   // 2. the level-2 groups' start states: at most 4, composed in order from s0 (M_3 = M_2^64)
   if (t < P) {
@@ -785,7 +732,7 @@ __global__ __launch_bounds__(64 * kUpperAggWaves<P>) void k_iir_scan_upper(uint6
     }
   }
   __syncthreads();
-  if (!own || !(e2 < E2)) return;
+  if (!(e2 < E2)) return;
   // 3. this wave's level-2 element start: M_2^r2 S_group + incl2[e2 - 1] (uniform across the wave)
   const int r2 = (int)(e2 % kGroup);
   const int q2 = (int)(e2 / kGroup);
@@ -883,8 +830,7 @@ static hipError_t run(const Coeffs& cf, S* xh, S* yh, const S* x, S* y, uint64_t
   const int lowest = F ? 1 : 0;  // levels scanned outside the chunk passes
   int rest = lowest;             // first level handled by the single-workgroup kernels
   while (rest <= levels && ceil_div<uint64_t>(E[rest], kGroup) > (uint64_t)kRestGroups) ++rest;
-  // with k_iir_scan_upper: that kernel alone (it folds level 1's up-sweep in, round 4)
-  const int stop = upper ? lowest : rest;
+  const int stop = upper ? 2 : rest;  // with k_iir_scan_upper: level 1's up-sweep, then that kernel
   for (int k = lowest; k < stop; ++k) {
     k_iir_up<A, P><<<(uint32_t)ceil_div<uint64_t>(E[k], kGroup), 64, 0, st>>>(elems(k), E[k], table(k), starts(k),
                                                                              elems(k + 1));
@@ -892,9 +838,9 @@ static hipError_t run(const Coeffs& cf, S* xh, S* yh, const S* x, S* y, uint64_t
   if constexpr (F) {
     if (upper) {
       const dim3 grid((uint32_t)ceil_div<uint64_t>(E[2], kUpperWaves), TileShape<S>::NC);
-      k_iir_scan_upper<P><<<grid, 64 * kUpperAggWaves<P>, 0, st>>>(
+      k_iir_scan_upper<P><<<grid, 64 * kUpperWaves, 0, st>>>(
           E[1], E[2], TileShape<S>::NC, table(1), table(2), levels >= 3 ? table(3) : nullptr,
-          reinterpret_cast<const double*>(elems(1)), reinterpret_cast<const double*>(s0),
+          reinterpret_cast<const double*>(elems(2)), reinterpret_cast<const double*>(s0),
           reinterpret_cast<double*>(starts(1)));
     }
   }

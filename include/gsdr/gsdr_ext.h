@@ -32,7 +32,7 @@ GSDR_C_LINKAGE GSDR_PUBLIC uint32_t gsdrNcoPhaseIncrement(
 
 /**
  * gsdrFirFC with an explicit kernel for decimation 4 (variant 0 = the default shape used by
- * gsdrFirFC; 1, 3, 4, 5, 24, 28 alternative workgroup / outputs-per-thread / chunk shapes; 7 = the
+ * gsdrFirFC; 1, 3, 4, 5, 24, 25, 26, 28 alternative workgroup / outputs-per-thread / chunk shapes; 7 = the
  * generic one-output-per-thread kernel; 8 = plain loads/stores; 9 = XCD-aware tile order; 10, 11 =
  * tile stored through LDS; 13 = exact-f32 matrix-core core, bit-identical to an ascending-tap fmaf
  * loop, tapCount <= 132; 14 = tile staged by LDS-DMA; >= 100 = ablation probes, not filters).

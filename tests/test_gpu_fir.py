@@ -114,7 +114,7 @@ def test_fir_restores_current_device(cuda):
 # Tile shapes of gsdrxFirFCVariant (fir_dispatch.hpp launch_d4_complex). The per-output MAC order of
 # the polyphase kernels depends only on (D, JC), so the JC = 16 shapes must equal variant 0 bit for
 # bit; the generic kernel (7) and the matrix-core core (13) sum in ascending tap order, like the oracle.
-VARIANTS_JC16 = [0, 1, 3, 8, 9, 10, 11, 14, 24, 28]
+VARIANTS_JC16 = [0, 1, 3, 8, 9, 10, 11, 14, 24, 25, 26, 28]
 VARIANTS_OTHER_ORDER = [4, 5]  # JC = 32 / JC = 8: own MAC order, normwise bar
 VARIANTS_ASCENDING = [7, 13]
 INT8_VARIANTS = [0, 1, 3, 4, 5, 7, 24, 28]  # launch_d4_int8

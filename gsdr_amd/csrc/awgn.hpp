@@ -89,15 +89,35 @@ __device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t
 // The table in LDS as two float planes R and S (all threads of the workgroup; the caller's barrier
 // publishes it): a normal's two loads then land in any registers, where (R, S) pairs had to be shuffled
 // apart for the packed fma of a symbol's two normals (three moves a symbol).
+// (GSDR_AWGN_PAIRS, a probe-build switch: the round-3 (R, S) pairs, one ds_read_b64 a normal.)
+#if defined(GSDR_AWGN_PAIRS) && !defined(GSDR_TUNING_PROBES)
+#error "GSDR_AWGN_PAIRS is a timing probe: probe builds only"
+#endif
 struct AwgnLds {
+#ifdef GSDR_AWGN_PAIRS
+  float2 rs[kAwgnTableSize];
+#else
   float r[kAwgnTableSize], s[kAwgnTableSize];
+#endif
 };
 __device__ __forceinline__ void awgn_load_table(AwgnLds& t, uint32_t nthreads) {
   for (uint32_t i = threadIdx.x; i < (uint32_t)kAwgnTableSize; i += nthreads) {
     const float2 e = c_awgn_table[i];
+#ifdef GSDR_AWGN_PAIRS
+    t.rs[i] = e;
+#else
     t.r[i] = e.x;
     t.s[i] = e.y;
+#endif
   }
+}
+__device__ __forceinline__ float awgn_fma(const AwgnLds& t, uint32_t i, float f) {
+#ifdef GSDR_AWGN_PAIRS
+  const float2 e = t.rs[i];
+  return fmaf(e.y, f, e.x);
+#else
+  return fmaf(t.s[i], f, t.r[i]);
+#endif
 }
 
 // m with its sign flipped where bit 31 of `sgn` is set: one v_bitop3_b32 (m ^ (sgn & 0x80000000))
@@ -112,7 +132,7 @@ __device__ __forceinline__ float awgn_normal_a(const AwgnLds& t, uint32_t a, uin
   const uint32_t x = (a << 1) | 1u;
   const uint32_t b = __float_as_uint((float)x);
   const uint32_t i = __builtin_amdgcn_ubfe(b, 18, 14) - 127u * 32u;
-  const float m = fmaf(t.s[i], (float)(b & 0x3ffffu), t.r[i]);
+  const float m = awgn_fma(t, i, (float)(b & 0x3ffffu));
   return awgn_sign(m, sgn);
 }
 
@@ -123,7 +143,7 @@ __device__ __forceinline__ float awgn_normal(const AwgnLds& t, uint32_t r) {
   // index (b >> 18) - 127 * 32: the exponent and the top 5 mantissa bits
   const uint32_t i = __builtin_amdgcn_ubfe(b, 18, 14) - 127u * 32u;
   // S is stored pre-scaled by 2^-18 (exact), so S f = S' (b & 0x3ffff) with the integer converted exactly
-  const float m = fmaf(t.s[i], (float)(b & 0x3ffffu), t.r[i]);
+  const float m = awgn_fma(t, i, (float)(b & 0x3ffffu));
   return awgn_sign(m, r << 11);
 }
 

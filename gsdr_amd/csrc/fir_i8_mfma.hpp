@@ -390,6 +390,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
   if (blockIdx.x < tiles) i8_load_granules<G, LM>(st, p, ((int64_t)blockIdx.x * C::KT - phase) * D + p.in_off);
   for (uint32_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
     const int64_t k_t = (int64_t)tile * C::KT - phase;  // a multiple of 16 in absolute output index
+    // the tile's outputs as 32-bit offsets from a uniform base: its writable range [lo, hi) (64-bit index
+    // arithmetic and compares per output had cost ~6 VALU instructions an output)
+    float2* __restrict__ out_t = out + k_t;
+    const uint32_t lo = k_t < 0 ? (uint32_t)(-k_t) : 0u;
+    const uint32_t hi = (int64_t)p.N - k_t < (int64_t)C::KT ? (uint32_t)((int64_t)p.N - k_t) : (uint32_t)C::KT;
     i8_store_planes<C::PADP>(st, lds, C::PLANE);
     __syncthreads();
     // the next tile's loads fly while this one is computed
@@ -415,17 +420,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
       for (int i = 0; i < 4; ++i) r[i] = oscale(acc[i]);
       const float g0 = lane_xor1(c ? r[0] : r[2]), g1 = lane_xor1(c ? r[1] : r[3]);
       const float4 o4 = c ? make_float4(g0, r[2], g1, r[3]) : make_float4(r[0], g0, r[1], g1);
-      const int64_t k = k_t + cbase + 16u * (uint32_t)b + 4u * (uint32_t)q + 2u * (uint32_t)c;
-      if (k >= 0 && (uint64_t)k + 1 < p.N) {
+      const uint32_t kr = cbase + 16u * (uint32_t)b + 4u * (uint32_t)q + 2u * (uint32_t)c;  // within the tile
+      if (kr >= lo && kr + 1 < hi) {
         if constexpr (OA) {
-          store16_nt(reinterpret_cast<float4*>(out + k), o4);
+          store16_nt(reinterpret_cast<float4*>(out_t + kr), o4);
         } else {
-          out[k] = make_float2(o4.x, o4.y);
-          out[k + 1] = make_float2(o4.z, o4.w);
+          out_t[kr] = make_float2(o4.x, o4.y);
+          out_t[kr + 1] = make_float2(o4.z, o4.w);
         }
       } else {
-        if (k >= 0 && (uint64_t)k < p.N) out[k] = make_float2(o4.x, o4.y);
-        if (k + 1 >= 0 && (uint64_t)(k + 1) < p.N) out[k + 1] = make_float2(o4.z, o4.w);
+        if (kr >= lo && kr < hi) out_t[kr] = make_float2(o4.x, o4.y);
+        if (kr + 1 >= lo && kr + 1 < hi) out_t[kr + 1] = make_float2(o4.z, o4.w);
       }
     }
     __syncthreads();  // every wave is done reading the tile's planes
@@ -565,6 +570,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
   if (blockIdx.x < tiles) i8_load_granules<4, LM>(st, p, ((int64_t)blockIdx.x * C::STRIDE - phase) * D + p.in_off);
   for (uint32_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
     const int64_t k_t = (int64_t)tile * C::STRIDE - phase;  // a multiple of 16 in absolute output index
+    // the tile's outputs as 32-bit offsets from a uniform base, writable in [lo, hi)
+    float* __restrict__ out_t = out + k_t;
+    const uint32_t lo = k_t < 0 ? (uint32_t)(-k_t) : 0u;
+    const uint32_t hi = (int64_t)p.N - k_t < (int64_t)C::STRIDE ? (uint32_t)((int64_t)p.N - k_t) : (uint32_t)C::STRIDE;
     i8_store_planes<C::PADP>(st, lds, C::PLANE);
     __syncthreads();
     // the next tile's loads fly while this one is computed
@@ -610,8 +619,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
                                    __uint_as_float((mi & b0mask) | (gi & ~b0mask)));
       const uint32_t rr = cbase + o_lane;  // this lane's output within the tile
       if constexpr (MODE == kModeAm) {
-        const int64_t k = k_t + rr;
-        if (k >= 0 && (uint64_t)k < p.N) out[k] = am_env(y);
+        if (rr >= lo && rr < hi) out_t[rr] = am_env(y);
       } else {
         ycur[ct] = y;
         if (ct == 0 && lane == 0u) wfirst[w] = y;  // output 0 of the wave's first C tile
@@ -663,10 +671,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
             const float2 zr = disc_product(u0, u1);
             ang[h] = atan2f(zr.y, zr.x);
           }
-          const int64_t k = k_t + rr[h];
-          if ((h == 0 || cb != ct) && rr[h] < (uint32_t)C::STRIDE && k >= 0 && (uint64_t)k < p.N) {
-            out[k] = p.fm_gain * ang[h];
-          }
+          if ((h == 0 || cb != ct) && rr[h] >= lo && rr[h] < hi) out_t[rr[h]] = p.fm_gain * ang[h];
         }
       }
     } else {

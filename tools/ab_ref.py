@@ -1,0 +1,109 @@
+#!/usr/bin/env python3
+"""Side-by-side timing of the working tree's libgsdr.so against an earlier build (development tool):
+    python tools/ab_ref.py build/ref_50fdf7b/libgsdr.so
+Each entry point on its bench shape, both libraries interleaved over ROUNDS rounds in one process on the same
+buffers (HIP events around back-to-back launches; min over rounds), so box-to-box spread cancels."""
+import ctypes
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from gsdr_amd.signals import lowpass_taps  # noqa: E402
+
+ROUNDS = int(os.environ.get("ROUNDS", "4"))
+REPS = int(os.environ.get("REPS", "30"))
+f, u32, i32, p, sz, u64 = ctypes.c_float, ctypes.c_uint32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64
+SIGS = {
+    "gsdrFirFC": [sz, p, sz, p, p, sz, i32, p],
+    "gsdrFmDemod": [f, f, f, f, u32, sz, p, sz, p, p, sz, i32, p],
+    "gsdrxFmDemodInt8": [f, f, f, f, u32, sz, p, sz, p, p, sz, i32, p],
+    "gsdrxAmDemodInt8": [f, f, f, u32, sz, p, sz, p, p, sz, i32, p],
+    "gsdrxFirFCInt8": [sz, p, sz, p, p, sz, i32, p],
+    "gsdrxQpsk256ModulateAwgn": [p, p, u32, u32, f, u64, u64, i32, p],
+    "gsdrQpsk256Demodulate": [p, p, u32, u32, i32, p],
+    "gsdrQpsk256InitConstellation": [u32, f, i32, p],
+    "gsdrIirFF": [p, p, sz, p, p, p, p, sz, i32, p],
+}
+
+
+def load(path):
+    lib = ctypes.CDLL(path)
+    for n, a in SIGS.items():
+        getattr(lib, n).argtypes = a
+        getattr(lib, n).restype = ctypes.c_int
+    return lib
+
+
+def main():
+    libs = [os.path.join(ROOT, "gsdr_amd", "libgsdr.so")] + sys.argv[1:]
+    L = [load(x) for x in libs]
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    g = torch.Generator(device=dev).manual_seed(7)
+    D, T, NO = 4, 127, 1 << 24
+    NI = (NO - 1) * D + T
+    taps = torch.from_numpy(lowpass_taps(T, 0.1)).to(dev)
+    xs = [(torch.rand(2 * NI, device=dev, generator=g) * 2 - 1).view(torch.complex64) for _ in range(2)]
+    x8s = [torch.randint(-100, 100, (2 * NI,), dtype=torch.int8, device=dev, generator=g) for _ in range(2)]
+    yc = torch.empty(NO, dtype=torch.complex64, device=dev)
+    yf = torch.empty(NO, dtype=torch.float32, device=dev)
+    n5 = 1 << 24
+    syms = torch.randint(0, 256, (n5,), dtype=torch.uint8, device=dev, generator=g)
+    rx = torch.empty(n5, dtype=torch.complex64, device=dev)
+    dec = torch.empty(n5, dtype=torch.uint8, device=dev)
+    from scipy import signal as sps
+
+    bb, aa = (torch.tensor(v, dtype=torch.float32, device=dev) for v in sps.butter(4, 0.1))
+    xi = torch.rand(n5, device=dev, generator=g)
+    yi = torch.empty_like(xi)
+    for lib in L:
+        assert lib.gsdrQpsk256InitConstellation(0, 1.0, 0, st) == 0
+    cases = {
+        "gsdrFirFC": lambda lib, k: lib.gsdrFirFC(D, taps.data_ptr(), T, xs[k % 2].data_ptr(), yc.data_ptr(), NO, 0, st),
+        "gsdrFmDemod": lambda lib, k: lib.gsdrFmDemod(1e6, 0.0, 1e5, 2e4, D, 0, taps.data_ptr(), T, xs[k % 2].data_ptr(),
+                                                      yf.data_ptr(), NO - 1, 0, st),
+        "gsdrxFirFCInt8": lambda lib, k: lib.gsdrxFirFCInt8(D, taps.data_ptr(), T, x8s[k % 2].data_ptr(), yc.data_ptr(),
+                                                            NO, 0, st),
+        "gsdrxFmDemodInt8": lambda lib, k: lib.gsdrxFmDemodInt8(1e6, 0.0, 1e5, 2e4, D, 0, taps.data_ptr(), T,
+                                                                x8s[k % 2].data_ptr(), yf.data_ptr(), NO - 1, 0, st),
+        "gsdrxAmDemodInt8": lambda lib, k: lib.gsdrxAmDemodInt8(1e6, 0.0, 1e5, D, 0, taps.data_ptr(), T,
+                                                                x8s[k % 2].data_ptr(), yf.data_ptr(), NO - 1, 0, st),
+        "gsdrxQpsk256ModulateAwgn": lambda lib, k: lib.gsdrxQpsk256ModulateAwgn(syms.data_ptr(), rx.data_ptr(), n5, 0,
+                                                                                0.02, 0x5EED0005, 0, 0, st),
+        "gsdrQpsk256Demodulate": lambda lib, k: lib.gsdrQpsk256Demodulate(rx.data_ptr(), dec.data_ptr(), n5, 0, 0, st),
+        "gsdrIirFF": lambda lib, k: lib.gsdrIirFF(bb.data_ptr(), aa.data_ptr(), 5, None, None, xi.data_ptr(),
+                                                  yi.data_ptr(), n5, 0, st),
+    }
+    only = os.environ.get("CASES")
+    res = {}
+    for r in range(ROUNDS):
+        for name, fn in cases.items():
+            if only and name not in only.split(","):
+                continue
+            for li, lib in enumerate(L):
+                for k in range(5):
+                    assert fn(lib, k) == 0
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for k in range(REPS):
+                    fn(lib, k)
+                e1.record()
+                torch.cuda.synchronize()
+                res.setdefault((name, li), []).append(e0.elapsed_time(e1) / REPS * 1e3)
+    names = [os.path.relpath(x, ROOT) for x in libs]
+    print(f"{'entry point':26s} " + " ".join(f"{n[:24]:>24s}" for n in names) + "   (min / median us)")
+    for name in cases:
+        if (name, 0) not in res:
+            continue
+        cols = []
+        for li in range(len(L)):
+            v = sorted(res[(name, li)])
+            cols.append(f"{v[0]:11.2f} / {v[len(v) // 2]:9.2f}")
+        print(f"{name:26s} " + " ".join(f"{c:>24s}" for c in cols), flush=True)
+
+
+if __name__ == "__main__":
+    main()

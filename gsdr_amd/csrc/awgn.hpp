@@ -165,7 +165,7 @@ __device__ __forceinline__ void awgn_block_words(uint64_t seed, uint64_t blk, ui
 
 // Both normals of slot `slot` when at least one of them is in the tail: the extension block, then the
 // tail-table value for each tail component (out of line: ~2e-4 of the lanes' blocks take it).
-__device__ __noinline__ float2 awgn_slot_tail(uint64_t seed, uint64_t blk, int slot, uint32_t r0, uint32_t r1,
+__device__ __forceinline__ float2 awgn_slot_tail(uint64_t seed, uint64_t blk, int slot, uint32_t r0, uint32_t r1,
                                              float2 g) {
   uint32_t x[4];
   philox4x32_10((uint32_t)blk, (uint32_t)(blk >> 32), 1u, 0u, (uint32_t)seed, (uint32_t)(seed >> 32), x);

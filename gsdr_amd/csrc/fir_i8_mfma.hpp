@@ -154,6 +154,16 @@ struct I8OutScale {
 // kernel (lanes 16 b + 4 q' outputs apart), P = 16 for the chain kernel (8 b). Round 3's P = 64 for both
 // took 2x (FIR) and 2.5x (chain) the conflict-free LDS cycles (PMC: 42 % of the chain's LDS-active cycles
 // were bank conflicts, profiles/r04_pmc_kernels.txt).
+// (GSDR_I8_FIR_PADP / GSDR_I8_CHAIN_PADP: probe-build overrides for layout A/B timing)
+#if !defined(GSDR_TUNING_PROBES) && (defined(GSDR_I8_FIR_PADP) || defined(GSDR_I8_CHAIN_PADP))
+#error "the int8 LDS pad periods are fixed outside the probe builds"
+#endif
+#ifndef GSDR_I8_FIR_PADP
+#define GSDR_I8_FIR_PADP 32
+#endif
+#ifndef GSDR_I8_CHAIN_PADP
+#define GSDR_I8_CHAIN_PADP 16
+#endif
 template <uint32_t P>
 __host__ __device__ constexpr uint32_t i8_addr(uint32_t idx) {
   return idx * 2u + (idx / P) * 16u;
@@ -314,7 +324,7 @@ struct I8Mfma {
   static constexpr int MAXT = 32 * MAXNS - 15 * D;
   static constexpr int SPAN = (KT - 16) * D + 32 * MAXNS;  // samples staged per tile
   static_assert(SPAN % 8 == 0, "staging moves 8 samples a lane");
-  static constexpr uint32_t PADP = 32;  // pad period (i8_addr)
+  static constexpr uint32_t PADP = GSDR_I8_FIR_PADP;  // pad period (i8_addr)
   __host__ __device__ static constexpr uint32_t addr(uint32_t idx) { return i8_addr<PADP>(idx); }
   // Q plane offset: = 128 (mod 256), so the Q columns' bank groups interleave the I columns'
   static constexpr uint32_t PLANE = (addr(SPAN) + 255u) / 256u * 256u + 128u;
@@ -469,7 +479,7 @@ struct I8ChainMfma {
   static constexpr int MAXT = 32 * MAXNS - 7 * D;  // 132
   static constexpr int SPAN = (KT - 8) * D + 32 * MAXNS;
   static_assert(SPAN % 4 == 0, "whole granules");
-  static constexpr uint32_t PADP = 16;  // pad period (i8_addr)
+  static constexpr uint32_t PADP = GSDR_I8_CHAIN_PADP;  // pad period (i8_addr)
   __host__ __device__ static constexpr uint32_t addr(uint32_t idx) { return i8_addr<PADP>(idx); }
   static constexpr uint32_t PLANE = (addr(SPAN) + 255u) / 256u * 256u + 128u;
   static constexpr uint32_t LDS_BYTES = PLANE + addr(SPAN);

@@ -190,6 +190,37 @@ def test_qpsk256_config5_round_trip(cuda, ctype, sigma):
     assert np.array_equal(got.cpu().numpy(), o.qpsk256_demod(table, rx_np, nthreads=_threads()))
 
 
+def test_qpsk256_awgn_tails_reach_beyond_five_sigma(cuda):
+    """the channel's noise must keep the Gaussian's tails (the 21-bit construction had none past
+    5.035 sigma). 2^24 symbols at sigma = 1 around point 0: the counts beyond 4.5 and 5.04 sigma over the
+    2^25 components follow erfc within Poisson bounds (5 sigma), the largest |g| is past the old cut, and a
+    tail-heavy slice is bit-identical to the oracle (which restates the extension)."""
+    import math
+
+    from gsdr_amd import ops
+
+    n, seed = 1 << 24, 0xABCDEF
+    ops.qpsk256_init(0, 1.0)
+    syms = torch.zeros(n, dtype=torch.uint8, device=cuda)
+    rx = ops.qpsk256_modulate_awgn(syms, 0, 1.0, seed, 0)
+    p0 = torch.tensor(complex(o.qpsk256_table(0, 1.0)[0]), dtype=torch.complex64, device=cuda)
+    g = torch.view_as_real(rx - p0).reshape(-1).abs()
+    comps = 2 * n
+    for t in (4.5, 5.04):
+        want = comps * math.erfc(t / math.sqrt(2.0))
+        got = int((g > t).sum())
+        assert abs(got - want) <= 5 * math.sqrt(want) + 2, (t, got, want)
+        assert got >= 4, (t, got)  # the 21-bit construction gave exactly 0 beyond 5.035
+    assert float(g.max()) > 5.04
+    # the symbols holding the largest components: the GPU's noisy values equal the oracle's bit for bit
+    idx = torch.topk(g, 64).indices.div(2, rounding_mode="floor").unique().cpu().numpy()
+    table = o.qpsk256_table(0, 1.0)
+    rx_np = rx.cpu().numpy()
+    for k in idx[:32]:
+        want = o.qpsk256_mod_awgn(table, np.zeros(1, np.uint8), 1.0, seed, int(k))
+        assert rx_np[k:k + 1].tobytes() == want.tobytes(), k
+
+
 @pytest.mark.parametrize("n", [1, 2, 3, 5, 6, 7, 1535, 1537, 4607, 4608, 4609, 100_003])  # 6 a lane step, 4608 a workgroup
 @pytest.mark.parametrize("first", [0, 1, 2, 2**32 - 1, 2**40 + 6, 2**33 + 3])  # first % 3: 0, 1, 2, 0, 1, 2
 def test_qpsk256_awgn_sizes_and_offsets(cuda, n, first):

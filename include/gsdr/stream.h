@@ -5,16 +5,18 @@
  * `firstSampleIndex` fm.h:48, am.h:30, fm.cu:202): to filter a stream in chunks, the caller must
  * re-supply the last taps-1 samples of the previous chunk and advance the NCO index itself. A
  * gsdrxStream object does that bookkeeping on the device: it keeps the samples the next output still
- * needs (fewer than one filter window) in a small device buffer, computes the outputs whose window
- * straddles the seam from that history plus the head of the new chunk, computes every other output
- * directly from the caller's chunk, and advances the absolute sample index that the NCO phase is
- * derived from.
+ * needs (fewer than one filter window) in a small device buffer, and each call is ONE kernel launch that
+ * reads the outputs whose window straddles the seam partly from that history (by offset) and every other
+ * output straight from the caller's chunk, while one workgroup of the same launch copies the next history;
+ * it advances the absolute sample index that the NCO phase is derived from. (Decimations served by the
+ * runtime-decimation or generic kernels take three launches: history + chunk head gathered into a seam
+ * buffer, then the seam outputs and the remaining outputs.)
  *
  * Contract: feeding a signal x[0..S) in chunks of any sizes (including 0 and chunks shorter than the
  * filter) produces, concatenated over the calls, exactly the outputs of ONE call of the underlying
  * entry point over x[0..S) with firstSampleIndex = the value given at creation -- bit for bit
- * (the seam and main launches use the same kernels as the single call, and the NCO phase is a
- * function of the absolute sample index). Output m is produced by the first call after which its
+ * (the launch runs the kernel the single call runs, whose per-output summation order does not depend on
+ * where a call or tile starts, and the NCO phase is a function of the absolute sample index). Output m is produced by the first call after which its
  * whole window has arrived: FIR/AM windows are taps samples, FM windows taps + decimation samples.
  *
  * Kinds: GSDRX_STREAM_FIR (gsdrFirFC), GSDRX_STREAM_FM (gsdrFmDemod), GSDRX_STREAM_AM (gsdrAmDemod).

@@ -63,6 +63,37 @@ def test_chunked_equals_monolithic(cuda, kind, D, int8):
     assert torch.equal(got.view(torch.float32), want.view(torch.float32))
 
 
+@pytest.mark.parametrize("kind,D,T,L,nchunks", [
+    ("fir", 4, 127, 20_000_000, 7),   # monolithic on 1,024-output tiles, the calls on 512-output tiles
+    ("fm", 4, 127, 12_000_000, 5),
+    ("am", 9, 127, 400_000, 6),       # runtime-decimation kernel: the three-launch seam plan
+    ("fir", 4, 300, 600_000, 4),      # longer filter, two tap chunks more
+    ("fir", 2, 127, 600_000, 9),
+])
+def test_one_launch_calls_equal_monolithic(cuda, kind, D, T, L, nchunks):
+    """Round 4: every float stream call on the tiled kernels is ONE launch (seam samples read from the
+    history buffer, next history copied by the launch). Large calls whose tile shape differs from the
+    monolithic call's (the per-output MAC order depends only on D and JC), a shape that keeps the seam plan
+    (D = 9), and a long filter: concatenated outputs equal one call bit for bit."""
+    from gsdr_amd.signals import fm_test_signal, lowpass_taps
+    from gsdr_amd.stream import Stream
+
+    n0 = 77_777
+    x = fm_test_signal(L, noise=0.02, n0=n0)
+    xd = torch.from_numpy(x).to(cuda)
+    taps = torch.from_numpy(lowpass_taps(T)).to(cuda)
+    want = monolithic(kind, xd, taps, D, n0, False)
+    s = Stream(kind, taps, D, FS, TUNE, CHAN, DEV, first_sample_index=n0)
+    rng = np.random.default_rng(L + D)
+    cuts = np.sort(rng.choice(np.arange(1, L), nchunks - 1, replace=False))
+    bounds = [0, *cuts.tolist(), L]
+    got = torch.cat([s.process(xd[a:b]).clone() for a, b in zip(bounds[:-1], bounds[1:])])
+    s.close()
+    torch.cuda.synchronize()
+    assert got.numel() == want.numel()
+    assert torch.equal(got.view(torch.float32), want.view(torch.float32))
+
+
 def test_tiny_chunks_and_skipping_decimation(cuda):
     """D > W: outputs skip samples; one-sample chunks throughout."""
     from gsdr_amd import ops

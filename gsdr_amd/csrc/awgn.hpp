@@ -100,9 +100,14 @@ struct AwgnLds {
   float r[kAwgnTableSize], s[kAwgnTableSize];
 #endif
 };
+// Entries below kAwgnTailIndex serve only tail components (a < 32 <=> x = 2 a + 1 < 64 <=> index < 6 * 32),
+// whose values the tail extension replaces: their R is NaN in LDS, so a tail component turns its symbol's
+// noisy output into NaN and one NaN test over a lane's outputs finds it (awgn_has_tail).
+constexpr uint32_t kAwgnTailIndex = 6 * 32;
 __device__ __forceinline__ void awgn_load_table(AwgnLds& t, uint32_t nthreads) {
   for (uint32_t i = threadIdx.x; i < (uint32_t)kAwgnTableSize; i += nthreads) {
-    const float2 e = c_awgn_table[i];
+    float2 e = c_awgn_table[i];
+    if (i < kAwgnTailIndex) e.x = __builtin_nanf("");
 #ifdef GSDR_AWGN_PAIRS
     t.rs[i] = e;
 #else
@@ -183,6 +188,45 @@ __device__ __forceinline__ float2 awgn_slot_tail(uint64_t seed, uint64_t blk, in
   if (awgn_in_tail(r0)) g.x = awgn_tail_normal(r0, e0);
   if (awgn_in_tail(r1)) g.y = awgn_tail_normal(r1, e1);
   return g;
+}
+
+// The 21-bit components of slot `slot`.
+__device__ __forceinline__ void awgn_slot_bits(const uint32_t (&w)[4], int slot, uint32_t& r0, uint32_t& r1) {
+  if (slot == 0) {
+    r0 = w[0] >> 11;
+    r1 = w[1] >> 11;
+  } else if (slot == 1) {
+    r0 = w[2] >> 11;
+    r1 = w[3] >> 11;
+  } else {
+    r0 = ((w[0] & 0x7ffu) << 10) | ((w[1] & 0x7ffu) >> 1);
+    r1 = ((w[2] & 0x7ffu) << 10) | ((w[3] & 0x7ffu) >> 1);
+  }
+}
+
+// The normal pair of slot `slot` from the main table only: exact unless a component is in the tail, where it
+// is NaN (awgn_has_tail tests a lane's outputs once, so the common path has no branch a slot).
+__device__ __forceinline__ float2 awgn_slot_main(const AwgnLds& tab, const uint32_t (&w)[4], int slot) {
+  if (slot < 2) {  // a = bits 11..30 of the word, the sign its bit 31
+    const uint32_t wa = w[2 * slot], wb = w[2 * slot + 1];
+    return make_float2(awgn_normal_a(tab, __builtin_amdgcn_ubfe(wa, 11, 20), wa),
+                       awgn_normal_a(tab, __builtin_amdgcn_ubfe(wb, 11, 20), wb));
+  }
+  uint32_t r0, r1;
+  awgn_slot_bits(w, 2, r0, r1);
+  return make_float2(awgn_normal(tab, r0), awgn_normal(tab, r1));
+}
+
+// Whether outputs y[0 .. K) computed from awgn_slot_main normals may hold a tail component: a NaN in their
+// sum (the tail entries' NaN R, kAwgnTailIndex). Also true for outputs that are NaN or overflow for other
+// reasons (a non-finite sigma); the caller's exact pass (awgn_slot_fix) then just reproduces them.
+template <int K>
+__device__ __forceinline__ bool awgn_has_tail(const float2 (&y)[K]) {
+  typedef float f2v __attribute__((ext_vector_type(2)));
+  f2v c = {y[0].x, y[0].y};
+#pragma unroll
+  for (int j = 1; j < K; ++j) c += f2v{y[j].x, y[j].y};
+  return __builtin_isnan(c.x + c.y);
 }
 
 // The normal pair of slot `slot` (0..2, compile-time after unrolling) of block `blk` (words w).

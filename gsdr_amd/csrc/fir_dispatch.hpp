@@ -316,7 +316,7 @@ hipError_t launch_multi_chain(const FirJob& j, const MultiParams& mp, hipStream_
 // int8 I/Q FIR on the matrix cores (k_fir_i8_mfma, fir_i8_mfma.hpp): D = 4, T <= 196; persistent
 // workgroups (their tap fragments are built once). The tile grid starts at output -out_phase, so the
 // staging granule and the output pairs are aligned per call from the pointers and the phase.
-template <int D, int NS, int BPC, int NCT>
+template <int D, int NS, int BPC, int NCT, int PF = 1>
 hipError_t launch_i8_mfma_nct(const FirJob& j, const FirParams& p, uint32_t ns, uint64_t tiles, uint32_t grid,
                               hipStream_t s) {
   using C = I8Mfma<D, NS, NCT>;
@@ -324,8 +324,8 @@ hipError_t launch_i8_mfma_nct(const FirJob& j, const FirParams& p, uint32_t ns, 
   const uintptr_t in0 = reinterpret_cast<uintptr_t>(j.in) + (uintptr_t)(2 * j.in_off) - 2u * D * p.out_phase;
   const bool oa = ((reinterpret_cast<uintptr_t>(j.out) - 8u * p.out_phase) % 16) == 0;
 #define GSDR_I8_LAUNCH(G, LM)                                                                                     \
-  (oa ? (k_fir_i8_mfma<D, NS, G, LM, true, BPC, NCT><<<dim3(grid), dim3(C::WG), 0, s>>>(p, ns, (uint32_t)tiles), 0) \
-      : (k_fir_i8_mfma<D, NS, G, LM, false, BPC, NCT><<<dim3(grid), dim3(C::WG), 0, s>>>(p, ns, (uint32_t)tiles), 0))
+  (oa ? (k_fir_i8_mfma<D, NS, G, LM, true, BPC, NCT, PF><<<dim3(grid), dim3(C::WG), 0, s>>>(p, ns, (uint32_t)tiles), 0) \
+      : (k_fir_i8_mfma<D, NS, G, LM, false, BPC, NCT, PF><<<dim3(grid), dim3(C::WG), 0, s>>>(p, ns, (uint32_t)tiles), 0))
   if (in0 % 16 == 0) {
     (void)GSDR_I8_LAUNCH(8, 1);
   } else if (in0 % 8 == 0) {
@@ -443,7 +443,10 @@ inline hipError_t launch_d4_int8(const FirJob& j, hipStream_t s) {
     case 41:  // matrix cores, 3 workgroups per CU: the default for D = 4
       return launch_i8_mfma<4, 3>(j, s);
     case 42:  // matrix cores, 3 workgroups per CU, 1,024-output tiles at every size (tile-shape sweep)
-    case 43: {  // the same with 512-output tiles
+    case 43:    // the same with 512-output tiles
+    case 44:    // 512-output tiles, 4 workgroups per CU
+    case 45:    // 512-output tiles, two tiles in flight a workgroup
+    case 46: {  // 512-output tiles, 4 workgroups per CU, two tiles in flight
       if (j.D != 4 || j.T < 1 || j.T > (size_t)I8Mfma<4, 6>::MAXT || (reinterpret_cast<uintptr_t>(j.out) % 8) != 0) {
         return hipErrorInvalidValue;
       }
@@ -454,9 +457,20 @@ inline hipError_t launch_d4_int8(const FirJob& j, hipStream_t s) {
       if (e != hipSuccess) return e;
       const uint64_t kt = j.variant == 42 ? (uint64_t)I8Mfma<4, 6, 2>::KT : (uint64_t)I8Mfma<4, 6, 1>::KT;
       const uint64_t t = ceil_div<uint64_t>(j.N + p.out_phase, kt);
-      const uint32_t grid = (uint32_t)std::min<uint64_t>(t, (uint64_t)cus * 3);
-      return j.variant == 42 ? launch_i8_mfma_nct<4, 6, 3, 2>(j, p, ns, t, grid, s)
-                             : launch_i8_mfma_nct<4, 6, 3, 1>(j, p, ns, t, grid, s);
+      const uint64_t bpc = (j.variant == 44 || j.variant == 46) ? 4 : 3;
+      const uint32_t grid = (uint32_t)std::min<uint64_t>(t, (uint64_t)cus * bpc);
+      switch (j.variant) {
+        case 42:
+          return launch_i8_mfma_nct<4, 6, 3, 2>(j, p, ns, t, grid, s);
+        case 44:
+          return launch_i8_mfma_nct<4, 6, 4, 1>(j, p, ns, t, grid, s);
+        case 45:
+          return launch_i8_mfma_nct<4, 6, 3, 1, 2>(j, p, ns, t, grid, s);
+        case 46:
+          return launch_i8_mfma_nct<4, 6, 4, 1, 2>(j, p, ns, t, grid, s);
+        default:
+          return launch_i8_mfma_nct<4, 6, 3, 1>(j, p, ns, t, grid, s);
+      }
     }
     default:
       return hipErrorInvalidValue;

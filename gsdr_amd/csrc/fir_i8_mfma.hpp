@@ -65,6 +65,31 @@ __device__ __forceinline__ bool split3(float v, __bf16& b1, __bf16& b2, __bf16& 
          bf16_normal_or_zero(b3);
 }
 
+// Tap parts in LDS for the A fragments: three bf16 rows (b1, b2, b3 of split3) of kI8TapPad zeros followed by
+// the parts of taps 0 .. 255 (zero past T). A lane's fragment for one K step is 8 consecutive taps, so it is one
+// 16-byte gather from a row (two 8-byte LDS reads) after one split a thread, where splitting the fragment
+// entries in every lane took 48 splits a lane (~3 us of VALU at the start of every launch).
+constexpr int kI8TapPad = 64;  // >= 15 D, the most negative tap index a fragment reaches (D = 4); 8-byte aligned rows
+constexpr int kI8TapRow = kI8TapPad + 256;
+__device__ __forceinline__ void i8_put_tap_parts(__bf16* parts, uint32_t tid, float v) {
+  __bf16 b1, b2, b3;
+  (void)split3(v, b1, b2, b3);  // exactness is checked by the caller's reduction
+  parts[kI8TapPad + tid] = b1;
+  parts[kI8TapRow + kI8TapPad + tid] = b2;
+  parts[2 * kI8TapRow + kI8TapPad + tid] = b3;
+  if (tid < (uint32_t)kI8TapPad) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) parts[k * kI8TapRow + tid] = (__bf16)0.0f;
+  }
+}
+// taps i0 .. i0 + 7 of one part row (i0 >= -kI8TapPad, i0 a multiple of 4)
+__device__ __forceinline__ gsdr_b8 i8_tap_row(const __bf16* row, int i0) {
+  const char* b = reinterpret_cast<const char*>(row + kI8TapPad + i0);
+  const gsdr_u2v lo = *reinterpret_cast<const gsdr_u2v*>(b), hi = *reinterpret_cast<const gsdr_u2v*>(b + 8);
+  const gsdr_u4v u = {lo.x, lo.y, hi.x, hi.y};
+  return __builtin_bit_cast(gsdr_b8, u);
+}
+
 // int8 component (bits [8 u, 8 u + 8) of w) as gsdrInt8ToNormFloat's numerator: clamp -128 to -127
 __device__ __forceinline__ __bf16 i8_bf16(uint32_t w, int u) {
   return (__bf16)(float)max((int)(w << (24 - 8 * u)) >> 24, -127);
@@ -151,9 +176,10 @@ struct I8OutScale {
 // LDS plane layout: 2 bytes a sample, a 16-byte pad after every P samples. P is chosen per kernel so the
 // B-fragment reads (ds_read_b128, 16 lanes a cycle in the lane groups of MI355X_MICROARCH.md section LDS) hit
 // 16 distinct 16-byte bank slots, with the Q plane 128 bytes (mod 256) past the I plane: P = 32 for the FIR
-// kernel (lanes 16 b + 4 q' outputs apart), P = 16 for the chain kernel (8 b). Round 3's P = 64 for both
-// took 2x (FIR) and 2.5x (chain) the conflict-free LDS cycles (PMC: 42 % of the chain's LDS-active cycles
-// were bank conflicts, profiles/r04_pmc_kernels.txt).
+// kernel (lanes 16 b + 4 q' outputs apart). The chain kernel's rows are 8 b apart: P = 16 is conflict-free
+// there but timed slower than P = 32 for FM in side-by-side runs (tools/ab_ref.py; AM equal), so it takes 32.
+// Round 3's P = 64 for both took 2x (FIR) and 2.5x (chain) the conflict-free LDS cycles (PMC: 42 % of the
+// chain's LDS-active cycles were bank conflicts, profiles/r04_pmc_kernels.txt).
 // (GSDR_I8_FIR_PADP / GSDR_I8_CHAIN_PADP: probe-build overrides for layout A/B timing)
 #if !defined(GSDR_TUNING_PROBES) && (defined(GSDR_I8_FIR_PADP) || defined(GSDR_I8_CHAIN_PADP))
 #error "the int8 LDS pad periods are fixed outside the probe builds"
@@ -162,7 +188,7 @@ struct I8OutScale {
 #define GSDR_I8_FIR_PADP 32
 #endif
 #ifndef GSDR_I8_CHAIN_PADP
-#define GSDR_I8_CHAIN_PADP 16
+#define GSDR_I8_CHAIN_PADP 32
 #endif
 template <uint32_t P>
 __host__ __device__ constexpr uint32_t i8_addr(uint32_t idx) {
@@ -335,8 +361,11 @@ struct I8Mfma {
 // G / LM: staging granule and load mode (I8Stage, i8_load_granules); OA: the output pairs (k, k + 1) are 16-byte aligned.
 // NCT: C tiles per wave and tile (4; 1 for short calls, whose few large tiles would leave most workgroup
 // slots idle -- an output's summation order does not depend on the tile size, only on its 16-output block)
-template <int D, int NS, int G, int LM, bool OA, int BPC, int NCT = 4>
+// PF: tiles in flight a workgroup (1: the next tile's loads fly while this one is computed; 2: the next two,
+// for short calls of small tiles, whose compute is too short to cover one tile's HBM latency)
+template <int D, int NS, int G, int LM, bool OA, int BPC, int NCT = 4, int PF = 1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC))) void k_fir_i8_mfma(FirParams p, uint32_t ns, uint32_t tiles) {
+  static_assert(PF == 1 || PF == 2, "one or two tiles in flight");
   using C = I8Mfma<D, NS, NCT>;
   __shared__ __attribute__((aligned(16))) char lds[C::LDS_BYTES];
   __shared__ float wmax[C::WG / 64];
@@ -347,6 +376,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
   const uint32_t T = p.T;
   const int64_t phase = (int64_t)p.out_phase;
   i8_copy_history(p);
+  // the first tiles' loads fly while the tap fragments are built
+  I8Stage<G, C::SPAN, C::WG> st, st2;
+  if (blockIdx.x < tiles) i8_load_granules<G, LM>(st, p, ((int64_t)blockIdx.x * C::KT - phase) * D + p.in_off);
+  if (PF == 2 && blockIdx.x + gridDim.x < tiles) {
+    i8_load_granules<G, LM>(st2, p, ((int64_t)(blockIdx.x + gridDim.x) * C::KT - phase) * D + p.in_off);
+  }
 
   // tap scale (T <= MAXT <= 256: one tap a thread); `bad` = some tap is not finite
   const float t = tid < T ? taps[tid] : 0.0f;
@@ -371,24 +406,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
     }
     return;
   }
-  // scaled taps in LDS (zero past T), then this lane's A fragments: row m = lane & 15, k = 8 (lane >> 4) + j
-  float* ldsT = reinterpret_cast<float*>(lds);
-  ldsT[tid] = ldexpf(t, sc);
+  // the scaled taps' parts in LDS (zero past T), then this lane's A fragments: row m = lane & 15,
+  // k = 8 (lane >> 4) + j, tap 32 s + k - D m (<= 255)
+  static_assert(D == 4, "tap rows gathered at 8-byte aligned offsets (D m a multiple of 4, 15 D <= kI8TapPad)");
+  static_assert(C::LDS_BYTES >= 3 * kI8TapRow * sizeof(__bf16), "tap rows fit the tile's LDS");
+  __bf16* parts = reinterpret_cast<__bf16*>(lds);
+  i8_put_tap_parts(parts, tid, ldexpf(t, sc));
   __syncthreads();
   gsdr_b8 a1[C::MAXNS], a2[C::MAXNS], a3[C::MAXNS];
   {
     const int m = (int)(lane & 15u), q = (int)(lane >> 4);
 #pragma unroll
     for (int s = 0; s < C::MAXNS; ++s) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int i = 32 * s + 8 * q + j - D * m;
-        __bf16 b1, b2, b3;
-        (void)split3(i >= 0 ? ldsT[i] : 0.0f, b1, b2, b3);  // i <= 255
-        a1[s][j] = b1;
-        a2[s][j] = b2;
-        a3[s][j] = b3;
-      }
+      const int i0 = 32 * s + 8 * q - D * m;
+      a1[s] = i8_tap_row(parts, i0);
+      a2[s] = i8_tap_row(parts + kI8TapRow, i0);
+      a3[s] = i8_tap_row(parts + 2 * kI8TapRow, i0);
     }
   }
   const I8OutScale oscale(sc);
@@ -396,20 +429,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
 
   const int n = (int)(lane & 15u), q = (int)(lane >> 4), c = n & 1, b = n >> 1;
   const char* bplane = lds + (c ? C::PLANE : 0u);
-  I8Stage<G, C::SPAN, C::WG> st;
-  if (blockIdx.x < tiles) i8_load_granules<G, LM>(st, p, ((int64_t)blockIdx.x * C::KT - phase) * D + p.in_off);
-  for (uint32_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+  auto run_tile = [&](uint32_t tile, I8Stage<G, C::SPAN, C::WG>& cur) {
     const int64_t k_t = (int64_t)tile * C::KT - phase;  // a multiple of 16 in absolute output index
     // the tile's outputs as 32-bit offsets from a uniform base: its writable range [lo, hi) (64-bit index
     // arithmetic and compares per output had cost ~6 VALU instructions an output)
     float2* __restrict__ out_t = out + k_t;
     const uint32_t lo = k_t < 0 ? (uint32_t)(-k_t) : 0u;
     const uint32_t hi = (int64_t)p.N - k_t < (int64_t)C::KT ? (uint32_t)((int64_t)p.N - k_t) : (uint32_t)C::KT;
-    i8_store_planes<C::PADP>(st, lds, C::PLANE);
+    i8_store_planes<C::PADP>(cur, lds, C::PLANE);
     __syncthreads();
-    // the next tile's loads fly while this one is computed
-    if (tile + gridDim.x < tiles) {
-      i8_load_granules<G, LM>(st, p, (k_t + (int64_t)gridDim.x * C::KT) * D + p.in_off);
+    // the loads of the tile PF rounds on fly while this one is computed
+    if (tile + PF * gridDim.x < tiles) {
+      i8_load_granules<G, LM>(cur, p, (k_t + (int64_t)(PF * gridDim.x) * C::KT) * D + p.in_off);
     }
 #pragma unroll 1
     for (int ct = 0; ct < C::NCT; ++ct) {
@@ -444,6 +475,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
       }
     }
     __syncthreads();  // every wave is done reading the tile's planes
+  };
+  if constexpr (PF == 1) {
+    for (uint32_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) run_tile(tile, st);
+  } else {  // the two register sets alternate (static indices: unrolled by two)
+    for (uint32_t tile = blockIdx.x; tile < tiles; tile += 2u * gridDim.x) {
+      run_tile(tile, st);
+      if (tile + gridDim.x >= tiles) break;
+      run_tile(tile + gridDim.x, st2);
+    }
   }
 }
 
@@ -499,6 +539,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
   const uint32_t T = p.T;
   const int64_t phase = (int64_t)p.out_phase;
   i8_copy_history(p);
+  // the first tile's loads fly while the tap fragments are built
+  I8Stage<4, C::SPAN, C::WG> st;
+  if (blockIdx.x < tiles) i8_load_granules<4, LM>(st, p, ((int64_t)blockIdx.x * C::STRIDE - phase) * D + p.in_off);
 
   // modulated taps t'_i = t_i e^{j 2 pi (i inc) / 2^32}
   const float t = tid < T ? taps[tid] : 0.0f;
@@ -531,25 +574,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
     }
     return;
   }
-  float* ldsT = reinterpret_cast<float*>(lds);
-  ldsT[tid] = ldexpf(tr, sc);
-  ldsT[C::WG + tid] = ldexpf(ti, sc);
+  // the parts of t'r and t'i in LDS (i8_put_tap_parts), then this lane's A fragments: tap 32 s + 8 q + j - D m
+  // (<= 159) of the real (rows 0-7) or imaginary (rows 8-15) taps
+  static_assert(C::LDS_BYTES >= 6 * kI8TapRow * sizeof(__bf16), "tap rows fit the tile's LDS");
+  __bf16* parts = reinterpret_cast<__bf16*>(lds);
+  i8_put_tap_parts(parts, tid, ldexpf(tr, sc));
+  i8_put_tap_parts(parts + 3 * kI8TapRow, tid, ldexpf(ti, sc));
   __syncthreads();
   gsdr_b8 a1[C::MAXNS], a2[C::MAXNS], a3[C::MAXNS];
   {
     const int m = (int)(lane & 7u), im = (int)((lane >> 3) & 1u), q = (int)(lane >> 4);
-    const float* tab = ldsT + (im ? C::WG : 0);
+    const __bf16* tab = parts + (im ? 3 * kI8TapRow : 0);
 #pragma unroll
     for (int s = 0; s < C::MAXNS; ++s) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int i = 32 * s + 8 * q + j - D * m;  // <= 159 < WG
-        __bf16 b1, b2, b3;
-        (void)split3(i >= 0 ? tab[i] : 0.0f, b1, b2, b3);
-        a1[s][j] = b1;
-        a2[s][j] = b2;
-        a3[s][j] = b3;
-      }
+      const int i0 = 32 * s + 8 * q - D * m;
+      a1[s] = i8_tap_row(tab, i0);
+      a2[s] = i8_tap_row(tab + kI8TapRow, i0);
+      a3[s] = i8_tap_row(tab + 2 * kI8TapRow, i0);
     }
   }
   // FM: the rotation the taps leave out, 2 pi (4 inc mod 2^32) / 2^32 in (-pi, pi]
@@ -576,8 +617,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
   const int nb_lane = (int)(16u * (((m_next >> 1) & 1u) * 2u + (m_next >> 2)) + 2u * (o_next >> 3) +
                             ((m_next ^ (m_next >> 1)) & 1u));
   float2 ycur[MODE == kModeFm ? C::NCT : 1];
-  I8Stage<4, C::SPAN, C::WG> st;
-  if (blockIdx.x < tiles) i8_load_granules<4, LM>(st, p, ((int64_t)blockIdx.x * C::STRIDE - phase) * D + p.in_off);
   for (uint32_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
     const int64_t k_t = (int64_t)tile * C::STRIDE - phase;  // a multiple of 16 in absolute output index
     // the tile's outputs as 32-bit offsets from a uniform base, writable in [lo, hi)

@@ -299,28 +299,49 @@ __global__ __launch_bounds__(kCBlock) void k_c256_mod_awgn(const uint8_t* __rest
     const uint64_t s = ws + (uint64_t)kAwgnSym * lane;  // this lane's first symbol (a multiple of 6)
     const bool whole = ws + kAwgnWaveSyms <= n;          // wave-uniform
     const uint64_t b0 = (first + s) / 3u;  // (first + s) % 3 == R3
-    uint32_t w[NB][4];
+    // the main-table normals and outputs of the lane's six symbols
+    auto load_syms = [&](uint8_t (&sym)[kAwgnSym]) {
+      if (whole && in_even) {  // three 2-byte loads (s is even)
+        const uint16_t* __restrict__ in2 = reinterpret_cast<const uint16_t*>(in + s);
 #pragma unroll
-    for (int b = 0; b < NB; ++b) awgn_block_words(seed, b0 + b, w[b]);
-    uint8_t sym[kAwgnSym];
-    if (whole && in_even) {  // three 2-byte loads (s is even)
-      const uint16_t* __restrict__ in2 = reinterpret_cast<const uint16_t*>(in + s);
+        for (int q = 0; q < kAwgnSym / 2; ++q) {
+          const uint16_t v = in2[q];
+          sym[2 * q] = (uint8_t)v;
+          sym[2 * q + 1] = (uint8_t)(v >> 8);
+        }
+      } else {
 #pragma unroll
-      for (int q = 0; q < kAwgnSym / 2; ++q) {
-        const uint16_t v = in2[q];
-        sym[2 * q] = (uint8_t)v;
-        sym[2 * q + 1] = (uint8_t)(v >> 8);
+        for (int j = 0; j < kAwgnSym; ++j) sym[j] = s + j < n ? in[s + j] : 0;
       }
-    } else {
-#pragma unroll
-      for (int j = 0; j < kAwgnSym; ++j) sym[j] = s + j < n ? in[s + j] : 0;
-    }
+    };
     float2 y[kAwgnSym];
+    {
+      uint32_t w[NB][4];
 #pragma unroll
-    for (int j = 0; j < kAwgnSym; ++j) {
-      const float2 g = awgn_slot(ntab, w[(R3 + j) / 3], (R3 + j) % 3, seed, b0 + (R3 + j) / 3);
-      const float2 p = tab[sym[j]];
-      y[j] = make_float2(p.x + sigma * g.x, p.y + sigma * g.y);
+      for (int b = 0; b < NB; ++b) awgn_block_words(seed, b0 + b, w[b]);
+      uint8_t sym[kAwgnSym];
+      load_syms(sym);
+#pragma unroll
+      for (int j = 0; j < kAwgnSym; ++j) {
+        const float2 g = awgn_slot_main(ntab, w[(R3 + j) / 3], (R3 + j) % 3);
+        const float2 p = tab[sym[j]];
+        y[j] = make_float2(p.x + sigma * g.x, p.y + sigma * g.y);
+      }
+    }
+    // a lane whose blocks hold a tail component (~4e-4 of the lanes: its outputs hold a NaN, awgn.hpp) redoes
+    // them exactly, regenerating its blocks and reloading its symbols (so neither stays live in the common path)
+    if (__builtin_expect(awgn_has_tail(y), 0)) {
+      uint32_t w[NB][4];
+#pragma unroll
+      for (int b = 0; b < NB; ++b) awgn_block_words(seed, b0 + b, w[b]);
+      uint8_t sym[kAwgnSym];
+      load_syms(sym);
+#pragma unroll
+      for (int j = 0; j < kAwgnSym; ++j) {
+        const float2 g = awgn_slot(ntab, w[(R3 + j) / 3], (R3 + j) % 3, seed, b0 + (R3 + j) / 3);
+        const float2 p = tab[sym[j]];
+        y[j] = make_float2(p.x + sigma * g.x, p.y + sigma * g.y);
+      }
     }
     if (whole && aligned) {
 #pragma unroll

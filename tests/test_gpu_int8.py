@@ -183,13 +183,13 @@ def test_chain_int8_misaligned_bit_identical(cuda, mode, D, offset_bytes):
 # Matrix-core int8 FIR (gsdrxFirFCInt8Variant 40 / 41, k_fir_i8_mfma): exact bf16 samples, taps scaled by a
 # power of two and split exactly into three bf16 parts, fp32 accumulation in the matrix core's order -> the
 # normwise bar against the oracle (not bit-identical to the ascending-order float path).
-@pytest.mark.parametrize("variant", [40, 41, 42, 43])
+@pytest.mark.parametrize("variant", [40, 41, 42, 43, 44, 45, 46])
 @pytest.mark.parametrize("T", [1, 2, 8, 63, 127, 128, 196])
 @pytest.mark.parametrize("N", [1, 2, 2047, 2048, 2049, 50000 + 3])
 def test_fir_int8_mfma_parity(cuda, variant, T, N):
     from gsdr_amd import ops
 
-    if variant in (42, 43) and T > 132:
+    if variant >= 42 and T > 132:
         pytest.skip("tile-size sweep variants cover T <= 132 (6 K steps)")
 
     D = 4
@@ -200,6 +200,21 @@ def test_fir_int8_mfma_parity(cuda, variant, T, N):
     y = host(ops.fir_variant(variant, dev(taps, cuda), dev(x8, cuda), D, N))
     xf = as_complex(o.int8_to_float(x8))
     assert normwise_err(y, o.fir(taps, xf, D, N), bound(taps, xf, D, N)) <= FLOAT_TOL
+
+
+@pytest.mark.parametrize("N", [100_001, 2_000_003])
+def test_fir_int8_mfma_tile_shapes_bit_identical(cuda, N):
+    """512-output tiles with 3 or 4 workgroups a CU and one or two tiles in flight (variants 43-46, several
+    rounds of tiles a workgroup at 2 M outputs) give the default's outputs bit for bit: an output's summation
+    order depends only on its 16-output block."""
+    from gsdr_amd import ops
+
+    D, T = 4, 127
+    x8 = dev(iq8((N - 1) * D + T, seed=N), cuda)
+    taps = dev((np.random.default_rng(5).standard_normal(T) / np.sqrt(T)).astype(np.float32), cuda)
+    want = ops.fir_variant(41, taps, x8, D, N).view(torch.float32)
+    for variant in (42, 43, 44, 45, 46):
+        assert torch.equal(ops.fir_variant(variant, taps, x8, D, N).view(torch.float32), want), variant
 
 
 @pytest.mark.parametrize("offset_bytes", [2, 6])

@@ -83,7 +83,8 @@ def main():
         for name, fn in cases.items():
             if only and name not in only.split(","):
                 continue
-            for li, lib in enumerate(L):
+            for li in [(r + x) % len(L) for x in range(len(L))]:  # the order rotates round by round
+                lib = L[li]
                 for k in range(5):
                     assert fn(lib, k) == 0
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -261,6 +261,21 @@ def test_qpsk256_awgn_pointer_alignment(cuda, in_off, out_off):
     assert out.cpu().numpy().tobytes() == want.tobytes()
 
 
+def test_qpsk256_awgn_overflowing_sigma_matches_oracle(cuda):
+    """sigma * g overflowing to +-inf: the tail test (a NaN in a lane's output sum, awgn.hpp) also fires on
+    lanes whose infinities cancel in the sum; their exact pass must reproduce the same outputs."""
+    from gsdr_amd import ops
+
+    ctype, seed, first, n = 0, 0x5EED0005, 5, 3 * 4608 + 17
+    ops.qpsk256_init(ctype, 1.0)
+    table = o.qpsk256_table(ctype, 1.0)
+    syms_np = np.random.default_rng(3).integers(0, 256, n, dtype=np.uint8)
+    for sigma in (1e38, 3.4e38):
+        rx = ops.qpsk256_modulate_awgn(dev(syms_np, cuda), ctype, sigma, seed, first).cpu().numpy()
+        assert rx.tobytes() == o.qpsk256_mod_awgn(table, syms_np, sigma, seed, first).tobytes()
+        assert np.isinf(rx.view(np.float32)).any()
+
+
 def test_qpsk256_awgn_zero_sigma_is_modulate(cuda):
     from gsdr_amd import GsdrError, ops
 

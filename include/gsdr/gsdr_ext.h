@@ -85,7 +85,9 @@ GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxFirFCInt8(
 
 /** gsdrxFirFCInt8 with an explicit decimation-4 tile shape (tuning sweep; -1 = default; 40 / 41 = the
  *  matrix-core kernel at 2 / 3 workgroups per CU; 42 / 43 = at 3 workgroups per CU with 1,024- / 512-output
- *  tiles at every size, tapCount <= 132). */
+ *  tiles at every size; 44 = 512-output tiles at 4 workgroups per CU; 45 / 46 = 512-output tiles at 3 / 4
+ *  workgroups per CU with two tiles in flight a workgroup; 42-46: tapCount <= 132, the default's outputs bit
+ *  for bit). */
 GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxFirFCInt8Variant(
     int variant,
     size_t decimation,

@@ -176,10 +176,10 @@ struct I8OutScale {
 // LDS plane layout: 2 bytes a sample, a 16-byte pad after every P samples. P is chosen per kernel so the
 // B-fragment reads (ds_read_b128, 16 lanes a cycle in the lane groups of MI355X_MICROARCH.md section LDS) hit
 // 16 distinct 16-byte bank slots, with the Q plane 128 bytes (mod 256) past the I plane: P = 32 for the FIR
-// kernel (lanes 16 b + 4 q' outputs apart). The chain kernel's rows are 8 b apart: P = 16 is conflict-free
-// there but timed slower than P = 32 for FM in side-by-side runs (tools/ab_ref.py; AM equal), so it takes 32.
-// Round 3's P = 64 for both took 2x (FIR) and 2.5x (chain) the conflict-free LDS cycles (PMC: 42 % of the
-// chain's LDS-active cycles were bank conflicts, profiles/r04_pmc_kernels.txt).
+// kernel (lanes 16 b + 4 q' outputs apart), P = 16 for the chain kernel (8 b). Round 3's P = 64 for both took
+// 2x (FIR) and 2.5x (chain) the conflict-free LDS cycles (PMC: 42 % of the chain's LDS-active cycles were bank
+// conflicts, profiles/r04_pmc_kernels.txt). The chain is VALU-bound: P = 16 / 32 / 64 time the same
+// (profiles/r04_ab_o.txt), and 16 keeps its LDS cycles lowest.
 // (GSDR_I8_FIR_PADP / GSDR_I8_CHAIN_PADP: probe-build overrides for layout A/B timing)
 #if !defined(GSDR_TUNING_PROBES) && (defined(GSDR_I8_FIR_PADP) || defined(GSDR_I8_CHAIN_PADP))
 #error "the int8 LDS pad periods are fixed outside the probe builds"
@@ -188,7 +188,7 @@ struct I8OutScale {
 #define GSDR_I8_FIR_PADP 32
 #endif
 #ifndef GSDR_I8_CHAIN_PADP
-#define GSDR_I8_CHAIN_PADP 32
+#define GSDR_I8_CHAIN_PADP 16
 #endif
 template <uint32_t P>
 __host__ __device__ constexpr uint32_t i8_addr(uint32_t idx) {

@@ -26,6 +26,7 @@ SIGS = {
     "gsdrQpsk256Demodulate": [p, p, u32, u32, i32, p],
     "gsdrQpsk256InitConstellation": [u32, f, i32, p],
     "gsdrIirFF": [p, p, sz, p, p, p, p, sz, i32, p],
+    "gsdrIirCC": [p, p, sz, p, p, p, p, sz, i32, p],
 }
 
 
@@ -59,6 +60,8 @@ def main():
     bb, aa = (torch.tensor(v, dtype=torch.float32, device=dev) for v in sps.butter(4, 0.1))
     xi = torch.rand(n5, device=dev, generator=g)
     yi = torch.empty_like(xi)
+    xic = torch.rand(2 * n5, device=dev, generator=g).view(torch.complex64)
+    yic = torch.empty_like(xic)
     for lib in L:
         assert lib.gsdrQpsk256InitConstellation(0, 1.0, 0, st) == 0
     cases = {
@@ -76,6 +79,8 @@ def main():
         "gsdrQpsk256Demodulate": lambda lib, k: lib.gsdrQpsk256Demodulate(rx.data_ptr(), dec.data_ptr(), n5, 0, 0, st),
         "gsdrIirFF": lambda lib, k: lib.gsdrIirFF(bb.data_ptr(), aa.data_ptr(), 5, None, None, xi.data_ptr(),
                                                   yi.data_ptr(), n5, 0, st),
+        "gsdrIirCC": lambda lib, k: lib.gsdrIirCC(bb.data_ptr(), aa.data_ptr(), 5, None, None, xic.data_ptr(),
+                                                  yic.data_ptr(), n5, 0, st),
     }
     only = os.environ.get("CASES")
     res = {}

@@ -181,7 +181,7 @@ struct I8OutScale {
 // conflicts, profiles/r04_pmc_kernels.txt). The chain is VALU-bound: P = 16 / 32 / 64 time the same
 // (profiles/r04_ab_o.txt), and 16 keeps its LDS cycles lowest.
 // (GSDR_I8_FIR_PADP / GSDR_I8_CHAIN_PADP: probe-build overrides for layout A/B timing)
-#if !defined(GSDR_TUNING_PROBES) && (defined(GSDR_I8_FIR_PADP) || defined(GSDR_I8_CHAIN_PADP))
+#if !defined(GSDR_TUNING_PROBES) && (defined(GSDR_I8_FIR_PADP) || defined(GSDR_I8_CHAIN_PADP) || defined(GSDR_I8_FM_PROBE))
 #error "the int8 LDS pad periods are fixed outside the probe builds"
 #endif
 #ifndef GSDR_I8_FIR_PADP
@@ -674,6 +674,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
         if (ct == 0 && lane == 0u) wfirst[w] = y;  // output 0 of the wave's first C tile
       }
     }
+#if defined(GSDR_I8_FM_PROBE) && GSDR_I8_FM_PROBE == 1
+    // timing probe (probe builds only): the FM tile without the neighbour exchange and the discriminator
+    if constexpr (MODE == kModeFm) {
+      __syncthreads();
+#pragma unroll
+      for (int ct = 0; ct < C::NCT; ++ct) {
+        const uint32_t rr = (w * C::NCT + (uint32_t)ct) * 64u + o_lane;
+        if (rr >= lo && rr < hi) out_t[rr] = ycur[ct].x + ycur[ct].y;
+      }
+    } else
+#endif
     if constexpr (MODE == kModeFm) {
       // One barrier for the planes (read by every wave's MFMAs) and the waves' first outputs; the next tile's
       // staging barrier orders the reads of wfirst below before its next writes. Every other neighbour
@@ -698,6 +709,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
       for (int ct = 0; ct < C::NCT; ct += 2) {
         const int cb = ct + 1 < C::NCT ? ct + 1 : ct;
         const float2 za = disc_product(ycur[ct], ynx[ct]), zb = disc_product(ycur[cb], ynx[cb]);
+#if defined(GSDR_I8_FM_PROBE) && GSDR_I8_FM_PROBE == 2
+        {  // timing probe (probe builds only): the exchange and the products, no angle
+          const uint32_t r0 = (w * C::NCT + (uint32_t)ct) * 64u + o_lane, r1 = (w * C::NCT + (uint32_t)cb) * 64u + o_lane;
+          if (r0 >= lo && r0 < hi) out_t[r0] = za.x + za.y;
+          if (cb != ct && r1 >= lo && r1 < hi) out_t[r1] = zb.x + zb.y;
+          continue;
+        }
+#endif
         const gsdr_f32x2 a2 = disc_angle2(za, zb) + gsdr_f32x2{dphi, dphi};
         float ang[2] = {a2.x, a2.y};
         const float2 zz[2] = {za, zb};

@@ -334,9 +334,9 @@ def fm_multi_gpu(torch, device, taps, rank, world, steps):
     argsets = [(fs, tune, chan, dev_hz, DECIM, 0, taps.data_ptr(), TAPS, x.data_ptr(), y.data_ptr(), n_fm,
                 device.index, stream) for x in xs]
     torch.cuda.synchronize()
-    barrier()
-    t = time_abi(torch, abi.lib.gsdrFmDemod, argsets, reps=steps)
+    t_solo, t = time_solo_then_all(torch, rank, lambda: time_abi(torch, abi.lib.gsdrFmDemod, argsets, reps=steps))
     t_max = reduce_max(t, device)
+    t_ranks = [r[0] for r in gather_rows(torch, [t], rank, world, device)]
     # parity of this rank's channel (batch 0), after the timed region
     assert abi.lib.gsdrFmDemod(*argsets[0]) == 0
     torch.cuda.synchronize()
@@ -353,13 +353,78 @@ def fm_multi_gpu(torch, device, taps, rank, world, steps):
     return {"config": "BASELINE configs[3]: one NCO + 127-tap FIR + FM channel (67,108,987 samples of config 3's "
                       "signal) per GPU, independent channels, no collective",
             "n_gpus": world, "us_per_launch_max_over_ranks": round(t_max * 1e6, 2),
+            "us_per_launch_per_rank": [round(v * 1e6, 2) for v in t_ranks],
             "aggregate_msamples_per_s": round(world * n_in / t_max / 1e6, 1),
+            "solo_us_per_launch_rank0": round(t_solo * 1e6, 2) if t_solo else None,
+            "solo_msamples_per_s_rank0": round(n_in / t_solo / 1e6, 1) if t_solo else None,
+            "scaling_efficiency": round(t_solo / t_max, 4) if t_solo else None,
+            "scaling_efficiency_def": "agg(n) / (n agg(1)) with agg(1) = rank 0's channel timed alone in this job "
+                                      "(every other rank idle at a barrier) just before the concurrent run",
             "parity_ok": [bool(r[0] == 1.0) for r in rows],
             "parity_max_wrapped_err_over_pi_g": [float(r[1]) for r in rows],
             "output_digest": [int(r[2]) for r in rows],
             "parity_check": "per rank, 4 x 4096 outputs of its own channel vs a float64 torch restatement of the "
                             "chain (fm_reference_windows), wrapped-angle bar 1e-5 of pi g; digest = sum of the "
                             "output's int32 bit patterns mod 2^48"}
+
+
+def rank_identity(torch, dev_index, backend, world):
+    """What this rank ran on, for the N > 1 line: host, the device's PCI domain:bus:device and UUID (from
+    the HIP runtime through torch), the process-group backend and its world size."""
+    import socket
+
+    p = torch.cuda.get_device_properties(dev_index)
+    pci = f"{int(p.pci_domain_id):04x}:{int(p.pci_bus_id):02x}:{int(p.pci_device_id):02x}"
+    return {"host": socket.gethostname(), "device_index": dev_index, "pci": pci, "uuid": str(getattr(p, "uuid", "")),
+            "name": p.name, "backend": backend, "world_size": world}
+
+
+def gather_objects(obj, world):
+    """Every rank's object, in rank order (one all_gather_object; the object itself when not distributed)."""
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()) or world == 1:
+        return [obj]
+    out = [None] * world
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def distinct_devices(idents):
+    """True when no two ranks report the same physical device (host + PCI address + UUID)."""
+    keys = [(d["host"], d["pci"], d["uuid"]) for d in idents]
+    return len(set(keys)) == len(keys)
+
+
+def validate_ranks(idents, world, rehearse):
+    """The N > 1 line's self-check: every rank reports the same backend and world size as rank 0's job, and the
+    ranks sit on distinct GPUs -- unless BENCH_REHEARSE=1, where ranks deliberately share one card (gloo).
+    Returns a list of problems (empty = valid)."""
+    bad = []
+    if len(idents) != world:
+        bad.append(f"{len(idents)} rank records for world size {world}")
+    if any(d["world_size"] != world for d in idents):
+        bad.append("ranks disagree on the world size")
+    if len({d["backend"] for d in idents}) != 1:
+        bad.append("ranks disagree on the process-group backend")
+    want = "gloo" if rehearse else "nccl"
+    if world > 1 and any(d["backend"] != want for d in idents):
+        bad.append(f"backend is not {want}")
+    if world > 1 and not rehearse and not distinct_devices(idents):
+        bad.append("two ranks report the same GPU")
+    return bad
+
+
+def time_solo_then_all(torch, rank, fn_time):
+    """Time fn_time() on rank 0 alone (every other rank idle at a barrier), then on all ranks at once. Returns
+    (solo seconds on rank 0 or None elsewhere, this rank's concurrent seconds). The solo figure is the in-job
+    N = 1 reference for the scaling efficiency agg(n) / (n agg(1)) = t_solo / t_max."""
+    barrier()
+    solo = fn_time() if rank == 0 else None
+    barrier()
+    t = fn_time()
+    barrier()
+    return solo, t
 
 
 def gather_rows(torch, vals, rank, world, device):
@@ -667,6 +732,11 @@ def main():
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=device)
+    backend = dist.get_backend() if world > 1 else "none"
+    idents = gather_objects(rank_identity(torch, dev_index, backend, world), world)
+    problems = validate_ranks(idents, world, rehearse)
+    if problems:
+        raise SystemExit(f"rank {rank}: invalid multi-GPU job: {'; '.join(problems)}: {idents}")
 
     from gsdr_amd import ops
     from gsdr_amd.signals import lowpass_taps
@@ -708,6 +778,20 @@ def main():
     torch.cuda.synchronize()
     settle = settle_clocks(torch, step, args.settle_max) if args.settle_max > 0 else 0
     barrier()
+    solo_fir_s = None
+    if world > 1:
+        # the in-job N = 1 reference: rank 0's K launches with every other rank idle at the barrier
+        def fir_k():
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            a.record()
+            for _ in range(args.steps):
+                step()
+            b.record()
+            torch.cuda.synchronize()
+            return a.elapsed_time(b) / args.steps * 1e-3
+
+        solo_fir_s, _ = time_solo_then_all(torch, rank, fir_k)
 
     # One HIP event pair around the K timed launches, on the launch stream: an event record between
     # launches is itself a ~10 us GPU command (timestamp + cache flush) and would inflate both numbers.
@@ -725,6 +809,7 @@ def main():
     wall_max = reduce_max(wall, device)
     kern_s = ev0.elapsed_time(ev1) / args.steps * 1e-3  # mean launch duration (back-to-back launches)
     kern_s_max = reduce_max(kern_s, device)
+    per_rank = gather_rows(torch, [kern_s, wall], rank, world, device)
     fm_multi = None
     if world > 1 and not args.no_secondary:
         fm_multi = fm_multi_gpu(torch, device, taps, rank, world, args.steps)
@@ -773,6 +858,18 @@ def main():
             "alg_tflops": round(ALG_FLOP / kern_s / 1e12, 2),
         },
     }
+    if world > 1:
+        line["ranks"] = [dict(d, rank=r, fir_kernel_us=round(p[0] * 1e6, 2), wall_ms=round(p[1] * 1e3, 3))
+                         for r, (d, p) in enumerate(zip(idents, per_rank))]
+        line["multi_gpu_check"] = {
+            "backend": backend, "world_size": world, "distinct_devices": distinct_devices(idents),
+            "solo_fir_kernel_us_rank0": round(solo_fir_s * 1e6, 2),
+            "fir_scaling_efficiency": round(solo_fir_s / kern_s_max, 4),
+            "fir_scaling_efficiency_def": "agg(n) / (n agg(1)) = t_solo / t_max: rank 0's K launches timed alone in this "
+                                          "job (other ranks idle at a barrier) over the slowest rank's mean launch in "
+                                          "the concurrent timed region",
+            "validated": "ranks report one backend and world size; device host + PCI + UUID distinct per rank"
+                         + (" (not required under BENCH_REHEARSE)" if rehearse else "")}
     if rehearse:
         line["rehearsal"] = "BENCH_REHEARSE=1: gloo, ranks sharing GPUs; not a measurement"
     if pmc:

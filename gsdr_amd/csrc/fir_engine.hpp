@@ -475,9 +475,10 @@ __device__ __forceinline__ void stage_tile(float4* __restrict__ lds, const InT* 
     // granule g, written as two partial-granule LDS stores (8-byte aligned pieces). The halo re-writes
     // the body's last granule whole, as for complex input.
     static_assert(!VEC && SH > 0 && SH < 4, "shifted real staging: 1..3 floats off 16-byte alignment");
-    // (a tile at S0 < SH would load SH floats before the caller's buffer -- inside in[0]'s 16-byte block, so
-    // it cannot fault, but it is out of bounds: that tile takes the per-granule loads below instead)
-    if (S0 >= (uint64_t)SH && S0 + (uint64_t)NG * G <= p.L) {
+    // (a tile less than SH samples past the start of the caller's buffer would load samples before it --
+    // inside its first 16-byte block, so it cannot fault, but it is out of bounds: that tile takes the
+    // per-granule loads below instead. The buffer starts at `in - in_off` on the streaming path.)
+    if ((int64_t)S0 + p.in_off >= (int64_t)SH && S0 + (uint64_t)NG * G <= p.L) {
       float* __restrict__ l1 = reinterpret_cast<float*>(lds);
       const float4* __restrict__ src = reinterpret_cast<const float4*>(in + S0 - SH);  // 16-byte aligned
 #pragma unroll
@@ -515,7 +516,8 @@ __device__ __forceinline__ void stage_tile(float4* __restrict__ lds, const InT* 
   } else if constexpr (SH != 0) {
     static_assert((std::is_same<InT, float2>::value || std::is_same<InT, Iq8>::value) && !VEC && SH == 1,
                   "shifted staging is for 8-byte-aligned complex or 2-byte-aligned int8 I/Q input");
-    if (S0 >= 1u && S0 + (uint64_t)NG * G <= p.L) {  // (S0 = 0 would load the sample before the buffer)
+    // (a tile starting at the caller's buffer, chunk = in - in_off, would load the sample before it)
+    if ((int64_t)S0 + p.in_off >= 1 && S0 + (uint64_t)NG * G <= p.L) {
       float2* __restrict__ l2 = reinterpret_cast<float2*>(lds);
 #pragma unroll
       for (int b0 = 0; b0 < BPT; b0 += SB) {

@@ -619,10 +619,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
   float2 ycur[MODE == kModeFm ? C::NCT : 1];
   for (uint32_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
     const int64_t k_t = (int64_t)tile * C::STRIDE - phase;  // a multiple of 16 in absolute output index
-    // the tile's outputs as 32-bit offsets from a uniform base, writable in [lo, hi)
+    // the tile's outputs as 32-bit offsets from a uniform base, writable in [out_lo, out_hi)
     float* __restrict__ out_t = out + k_t;
-    const uint32_t lo = k_t < 0 ? (uint32_t)(-k_t) : 0u;
-    const uint32_t hi = (int64_t)p.N - k_t < (int64_t)C::STRIDE ? (uint32_t)((int64_t)p.N - k_t) : (uint32_t)C::STRIDE;
+    const uint32_t out_lo = k_t < 0 ? (uint32_t)(-k_t) : 0u;
+    const uint32_t out_hi = (int64_t)p.N - k_t < (int64_t)C::STRIDE ? (uint32_t)((int64_t)p.N - k_t) : (uint32_t)C::STRIDE;
     i8_store_planes<C::PADP>(st, lds, C::PLANE);
     __syncthreads();
     // the next tile's loads fly while this one is computed
@@ -668,7 +668,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
                                    __uint_as_float((mi & b0mask) | (gi & ~b0mask)));
       const uint32_t rr = cbase + o_lane;  // this lane's output within the tile
       if constexpr (MODE == kModeAm) {
-        if (rr >= lo && rr < hi) out_t[rr] = am_env(y);
+        if (rr >= out_lo && rr < out_hi) out_t[rr] = am_env(y);
       } else {
         ycur[ct] = y;
         if (ct == 0 && lane == 0u) wfirst[w] = y;  // output 0 of the wave's first C tile
@@ -681,7 +681,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
 #pragma unroll
       for (int ct = 0; ct < C::NCT; ++ct) {
         const uint32_t rr = (w * C::NCT + (uint32_t)ct) * 64u + o_lane;
-        if (rr >= lo && rr < hi) out_t[rr] = ycur[ct].x + ycur[ct].y;
+        if (rr >= out_lo && rr < out_hi) out_t[rr] = ycur[ct].x + ycur[ct].y;
       }
     } else
 #endif
@@ -712,8 +712,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
 #if defined(GSDR_I8_FM_PROBE) && GSDR_I8_FM_PROBE == 2
         {  // timing probe (probe builds only): the exchange and the products, no angle
           const uint32_t r0 = (w * C::NCT + (uint32_t)ct) * 64u + o_lane, r1 = (w * C::NCT + (uint32_t)cb) * 64u + o_lane;
-          if (r0 >= lo && r0 < hi) out_t[r0] = za.x + za.y;
-          if (cb != ct && r1 >= lo && r1 < hi) out_t[r1] = zb.x + zb.y;
+          if (r0 >= out_lo && r0 < out_hi) out_t[r0] = za.x + za.y;
+          if (cb != ct && r1 >= out_lo && r1 < out_hi) out_t[r1] = zb.x + zb.y;
           continue;
         }
 #endif
@@ -739,7 +739,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC)))
             const float2 zr = disc_product(u0, u1);
             ang[h] = atan2f(zr.y, zr.x);
           }
-          if ((h == 0 || cb != ct) && rr[h] >= lo && rr[h] < hi) out_t[rr[h]] = p.fm_gain * ang[h];
+          if ((h == 0 || cb != ct) && rr[h] >= out_lo && rr[h] < out_hi) out_t[rr[h]] = p.fm_gain * ang[h];
         }
       }
     } else {

@@ -46,3 +46,20 @@ def test_bench_two_ranks_rehearsal(cuda):
     assert fm["parity_ok"] == [True, True], fm
     assert all(e <= 1e-5 for e in fm["parity_max_wrapped_err_over_pi_g"])
     assert len(fm["output_digest"]) == 2 and fm["output_digest"][0] != fm["output_digest"][1]  # independent channels
+    # the line validates itself: per-rank device identity, backend, world size, per-rank times, in-job N = 1 figure
+    ranks = line["ranks"]
+    assert [r["rank"] for r in ranks] == [0, 1]
+    assert all(r["backend"] == "gloo" and r["world_size"] == 2 for r in ranks)
+    assert all(r["fir_kernel_us"] > 0 and r["wall_ms"] > 0 for r in ranks)
+    # rehearsal: both ranks on cuda:0, so the identities coincide -- accepted only because of the flag
+    assert ranks[0]["pci"] == ranks[1]["pci"] and ranks[0]["uuid"] == ranks[1]["uuid"]
+    chk = line["multi_gpu_check"]
+    assert chk["backend"] == "gloo" and chk["world_size"] == 2 and chk["distinct_devices"] is False
+    assert chk["solo_fir_kernel_us_rank0"] > 0 and 0 < chk["fir_scaling_efficiency"] < 10
+    assert max(r["fir_kernel_us"] for r in ranks) == pytest.approx(line["roofline"]["kernel_us_max_over_ranks"], rel=1e-3)
+    assert len(fm["us_per_launch_per_rank"]) == 2 and all(v > 0 for v in fm["us_per_launch_per_rank"])
+    assert max(fm["us_per_launch_per_rank"]) == pytest.approx(fm["us_per_launch_max_over_ranks"], rel=1e-3)
+    assert fm["solo_us_per_launch_rank0"] > 0
+    assert fm["scaling_efficiency"] == pytest.approx(fm["solo_us_per_launch_rank0"] / fm["us_per_launch_max_over_ranks"],
+                                                     rel=1e-2)
+

@@ -190,3 +190,60 @@ def test_iir_beyond_2_31_samples(cuda, cplx):
         got = y[k0:k1].cpu().numpy()
         e = float(np.max(np.abs(got - want))) / max(1.0, float(np.max(np.abs(want))))
         assert e <= 1e-6, (k0, e)
+
+
+def periodic_fm_int8(n_in, cuda, seed):
+    """Config 3's signal quantised to int8 I/Q (x 100) at any length: its clean part (carrier 0.1 fs, tone
+    0.001 fs, deviation 0.02 fs) repeats every 1000 samples, so one period is tiled; the noise (uniform
+    integers in [-5, 5] per component) is drawn chunk by chunk on the device."""
+    idx = torch.arange(1000, dtype=torch.float64)
+    ph = 2 * np.pi * 0.1 * idx + 20.0 * torch.sin(2 * np.pi * 0.001 * idx)
+    period = torch.round(torch.view_as_real(torch.polar(torch.ones_like(ph), ph)).reshape(-1) * 100).to(torch.int16)
+    period = period.to(cuda)
+    x8 = torch.empty(2 * n_in, dtype=torch.int8, device=cuda)
+    g = torch.Generator(device=cuda).manual_seed(seed)
+    chunk = 2000 * (1 << 16)  # a multiple of the period's 2000 bytes
+    for s in range(0, 2 * n_in, chunk):
+        e = min(s + chunk, 2 * n_in)
+        base = period.repeat(chunk // 2000)[:e - s]
+        noise = torch.randint(-5, 6, (e - s,), dtype=torch.int16, device=cuda, generator=g)
+        x8[s:e] = torch.clamp(base + noise, -128, 127).to(torch.int8)
+    return x8
+
+
+def test_int8_fir_and_fm_beyond_2_31_samples(cuda):
+    """gsdrxFirFCInt8 and gsdrxFmDemodInt8 (D = 4, T = 127: the matrix-core kernels, whose output indexing is
+    32-bit relative to each tile) over 2^31 + 143 int8 I/Q samples (4.3 GB in): windows at 2^30 and 2^31
+    input samples and at the end, against the oracle on the converted samples (normwise for the FIR,
+    wrapped angle for the FM chain, firstSampleIndex of each window = n0 + k0 D)."""
+    from gsdr_amd import ops
+    from gsdr_amd.signals import lowpass_taps
+
+    from helpers import wrapped_angle_err
+
+    D, T = 4, 127
+    n_out = (1 << 29) + 5
+    n_in = (n_out - 1) * D + T
+    x8 = periodic_fm_int8(n_in, cuda, 21)
+    taps_np = lowpass_taps(T, 0.1)
+    td = torch.from_numpy(taps_np).to(cuda)
+    y = ops.fir(td, x8, D, n_out)
+    torch.cuda.synchronize()
+    crossings = [1 << 28, 1 << 29, (1 << 29) - (T // D)]  # output k reads samples from 4k: 2^30, 2^31
+    for k0, k1 in windows(n_out, crossings):
+        xs = o.int8_to_float(x8[2 * k0 * D:2 * ((k1 - 1) * D + T)].cpu().numpy()).view(np.complex64)
+        want = o.fir(taps_np, xs, D, k1 - k0)
+        err = normwise_err(y[k0:k1].cpu().numpy(), want, o.fir_bound_fc(taps_np, xs, D, k1 - k0))
+        assert err <= FLOAT_TOL, ("fir", k0, err)
+    del y
+    torch.cuda.empty_cache()
+    fs, tune, chan, dhz, n0 = 1.0e6, 0.0, 1.0e5, 2.0e4, (1 << 32) + 11
+    n_fm = (n_in - T) // D
+    fm = ops.fm_demod(x8, td, fs, tune, chan, dhz, D, n0, n_fm)
+    torch.cuda.synchronize()
+    g = fs / (2 * np.pi * dhz)
+    for k0, k1 in windows(n_fm, crossings):
+        xs = o.int8_to_float(x8[2 * k0 * D:2 * (k1 * D + T)].cpu().numpy()).view(np.complex64)
+        want = o.fm_demod(xs, taps_np, fs, tune, chan, dhz, D, n0 + k0 * D, k1 - k0)
+        err = wrapped_angle_err(fm[k0:k1].cpu().numpy(), want, g)
+        assert err <= FLOAT_TOL, ("fm", k0, err)

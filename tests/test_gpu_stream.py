@@ -66,6 +66,8 @@ def test_chunked_equals_monolithic(cuda, kind, D, int8):
 @pytest.mark.parametrize("kind,D,T,L,nchunks", [
     ("fir", 4, 127, 20_000_000, 7),   # monolithic on 1,024-output tiles, the calls on 512-output tiles
     ("fm", 4, 127, 12_000_000, 5),
+    ("fm", 4, 127, 20_000_000, 5),    # monolithic FM / AM above the R = 4 threshold too
+    ("am", 4, 127, 20_000_000, 6),
     ("am", 9, 127, 400_000, 6),       # runtime-decimation kernel: the three-launch seam plan
     ("fir", 4, 300, 600_000, 4),      # longer filter, two tap chunks more
     ("fir", 2, 127, 600_000, 9),
@@ -82,6 +84,11 @@ def test_one_launch_calls_equal_monolithic(cuda, kind, D, T, L, nchunks):
     x = fm_test_signal(L, noise=0.02, n0=n0)
     xd = torch.from_numpy(x).to(cuda)
     taps = torch.from_numpy(lowpass_taps(T)).to(cuda)
+    if L >= 20_000_000:
+        # the monolithic call must run the 1,024-output (R = 4) tiles: launch_poly_d4 keeps R = 2 below
+        # 3 * CUs * 4 tiles of 1,024 outputs
+        cus = torch.cuda.get_device_properties(cuda).multi_processor_count
+        assert -(-(L // D) // 1024) > 3 * cus * 4, (L, cus)
     want = monolithic(kind, xd, taps, D, n0, False)
     s = Stream(kind, taps, D, FS, TUNE, CHAN, DEV, first_sample_index=n0)
     rng = np.random.default_rng(L + D)

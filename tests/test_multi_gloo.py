@@ -46,7 +46,15 @@ def worker(rank, world, port, q):
         # bench's own gather of the per-rank parity flags / digests (fm_multi_gpu)
         rows = bench.gather_rows(torch, [float(rank == rank), 0.5 * rank, float(10 + rank)], rank, world,
                                  torch.device("cpu"))
-        q.put((rank, seed, tmax, [float(g) for g in gathered], rows))
+        # the N > 1 line's self-check: per-rank identities gathered in rank order (each rank claims its own
+        # device here, as the GPU job does with one card per rank)
+        ident = {"host": "h", "device_index": rank, "pci": f"0000:{rank + 1:02x}:00", "uuid": f"u{rank}",
+                 "name": "n", "backend": dist.get_backend(), "world_size": dist.get_world_size()}
+        idents = bench.gather_objects(ident, world)
+        problems = bench.validate_ranks(idents, world, rehearse=True)
+        # rank 0 alone, then all ranks: the solo figure exists on rank 0 only
+        solo, conc = bench.time_solo_then_all(torch, rank, lambda: 1.0 + rank)
+        q.put((rank, seed, tmax, [float(g) for g in gathered], rows, idents, problems, solo, conc))
     finally:
         dist.destroy_process_group()
 
@@ -71,6 +79,36 @@ def test_two_rank_channels_and_timing():
     assert digests == results[1][3] and digests[0] != digests[1]  # channels really differ
     for r in results:  # every rank holds every rank's row, in rank order
         assert r[4] == [[1.0, 0.0, 10.0], [1.0, 0.5, 11.0]]
+        assert [d["pci"] for d in r[5]] == ["0000:01:00", "0000:02:00"] and r[6] == []
+    assert results[0][7] == 1.0 and results[1][7] is None
+    assert [r[8] for r in results] == [1.0, 2.0]
+
+
+def _ident(rank, pci, backend="nccl", world=2, host="h"):
+    return {"host": host, "device_index": rank, "pci": pci, "uuid": "u" + pci, "name": "MI355X", "backend": backend,
+            "world_size": world}
+
+
+def test_validate_ranks_rules():
+    """bench.validate_ranks: distinct GPUs required for a measured N > 1 line, shared ones allowed only under the
+    rehearsal flag; backend and world size must agree across ranks."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    good = [_ident(0, "0000:05:00"), _ident(1, "0000:15:00")]
+    assert bench.validate_ranks(good, 2, rehearse=False) == []
+    shared = [_ident(0, "0000:05:00"), _ident(1, "0000:05:00")]
+    assert any("same GPU" in p for p in bench.validate_ranks(shared, 2, rehearse=False))
+    assert bench.validate_ranks([dict(d, backend="gloo") for d in shared], 2, rehearse=True) == []
+    # same PCI address on two hosts is two GPUs
+    assert bench.validate_ranks([_ident(0, "0000:05:00", host="a"), _ident(1, "0000:05:00", host="b")], 2,
+                                rehearse=False) == []
+    assert bench.validate_ranks([_ident(0, "0000:05:00"), _ident(1, "0000:15:00", world=3)], 2, rehearse=False)
+    assert bench.validate_ranks([_ident(0, "0000:05:00"), _ident(1, "0000:15:00", backend="gloo")], 2,
+                                rehearse=False)
+    assert bench.validate_ranks(good, 2, rehearse=True)  # a rehearsal must run over gloo
+    assert bench.validate_ranks(good[:1], 2, rehearse=False)  # a missing rank
+    assert bench.validate_ranks([_ident(0, "0000:05:00", backend="none", world=1)], 1, rehearse=False) == []
 
 
 def test_fm_reference_windows_matches_oracle():

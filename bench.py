@@ -489,8 +489,15 @@ def secondary_configs(torch, ops, device, taps):
                                     kind=0, fmt=0, chunk_counts=(1, 8, 32), label="config 2's complex float channel "
                                     "through gsdrxStream (CF32 FIR, D = 4), C chunks a pass")
     out["fm_stream"] = stream_rate(torch, abi, device, taps, xs, stream, out["fm_chain"]["us_per_launch"] * 1e-6,
-                                   kind=1, fmt=0, chunk_counts=(1, 8, 32), label="config 3's channel through "
-                                   "gsdrxStream (CF32 FM chain, D = 4), C chunks a pass")
+                                   kind=1, fmt=0, chunk_counts=(1, 8, 32), call_sizes=(1 << 16, 1 << 18, 1 << 20),
+                                   label="config 3's channel through gsdrxStream (CF32 FM chain, D = 4), C chunks a "
+                                   "pass or receiver-sized calls of 2^16 / 2^18 / 2^20 samples")
+    # multi-channel stream (rows 1 x 3): 8 FM channels of one RF input, 2^20-sample calls, one grouped launch a call
+    out["fm_stream_multi_8ch"] = stream_rate(
+        torch, abi, device, taps, xs, stream, out["fm_chain"]["us_per_launch"] * 1e-6, kind=1, fmt=0, chunk_counts=(1,),
+        call_sizes=(1 << 20,), channels=8,
+        label="8 FM channels of config 3's input through one gsdrxStreamCreateMulti stream (CF32, D = 4): one grouped "
+              "launch a call")
     del xs
     # int8 I/Q front end fused into the filter: 2 instead of 8 input bytes per sample; the FM chain gets
     # config 3's signal quantised to int8 (x 100), consecutive batches of one channel
@@ -524,6 +531,10 @@ def secondary_configs(torch, ops, device, taps):
     out["fir_int8_stream"] = stream_rate(torch, abi, device, taps, x8s, stream, t, kind=0, fmt=1, chunk_counts=(1, 2, 8),
                                          label="config 2's int8 I/Q channel through gsdrxStream (CS8 FIR, D = 4), C "
                                          "chunks a pass")
+    out["fm_int8_stream"] = stream_rate(torch, abi, device, taps, x8s, stream, out["fm_chain_int8"]["us_per_launch"] * 1e-6,
+                                        kind=1, fmt=1, chunk_counts=(1, 8), call_sizes=(1 << 16, 1 << 18, 1 << 20),
+                                        label="config 3's int8 I/Q channel through gsdrxStream (CS8 FM chain, D = 4), "
+                                        "C chunks a pass or receiver-sized calls")
     del x8s, yf
     # true recursive IIR: 4th-order Butterworth over 2^24 samples
     from scipy import signal as sps
@@ -631,28 +642,43 @@ def out_fir_call(torch, abi, device, taps, xs, stream):
     return time_abi(torch, abi.lib.gsdrFirFC, argsets)
 
 
-def stream_rate(torch, abi, device, taps, xs, stream, t_call, kind, fmt, chunk_counts, label):
+def stream_rate(torch, abi, device, taps, xs, stream, t_call, kind, fmt, chunk_counts, label, call_sizes=(),
+                channels=1):
     """SURVEY.md 8(f) row 1 (and row 2 for int8 I/Q): a 64 M-sample channel fed through a gsdrxStream in C
     equal chunks per pass, passes rotating over the batches, against one call of the entry point (t_call).
     Every gsdrxStreamProcess call is ONE launch of the kernel one monolithic call runs (seam samples from
     the history buffer, next history written by the launch: the int8 matrix-core kernels since round 3,
     the float tiled kernels since round 4), so the difference is the per-launch fixed cost times C and the
-    host's issue time per call (host_us_per_call, measured over the same loop)."""
+    host's issue time per call (host_us_per_call, measured over the same loop). call_sizes: passes in calls of
+    that many samples (receiver-sized chunks); channels > 1: a gsdrxStreamCreateMulti stream of that many FM
+    channels of the same input."""
     import ctypes
+
+    import numpy as np
 
     res = {"config": label, "single_call_us": round(t_call * 1e6, 2)}
     sb = 2 if fmt == 1 else 8
-    y = torch.empty(N_OUT + 1024, dtype=torch.complex64, device=device)  # a call can emit the history's outputs too
-    yp, ycap = y.data_ptr(), y.numel()
+    # a call can emit the history's outputs too; a C-channel stream writes channel c at c * capacity
+    ycap = N_OUT + 1024
+    y = torch.empty(channels * ycap, dtype=torch.complex64 if kind == 0 else torch.float32, device=device)
+    yp = y.data_ptr()
     written = ctypes.c_size_t()
     wref = ctypes.byref(written)
     f = ctypes.c_float
-    for chunks in chunk_counts:
+    plan = [(c, f"{c}_chunks", N_IN // c) for c in chunk_counts]
+    plan += [(-(-N_IN // size), f"per_call_{size}_samples", size) for size in call_sizes]
+    for chunks, name, cs in plan:
         h = ctypes.c_void_p()
-        rc = abi.lib.gsdrxStreamCreate(ctypes.byref(h), kind, fmt, DECIM, taps.data_ptr(), TAPS, f(1.0e6), f(0.0),
-                                       f(1.0e5), f(2.0e4), 0, device.index)
+        if channels == 1:
+            rc = abi.lib.gsdrxStreamCreate(ctypes.byref(h), kind, fmt, DECIM, taps.data_ptr(), TAPS, f(1.0e6), f(0.0),
+                                           f(1.0e5), f(2.0e4), 0, device.index)
+        else:
+            chans = (f * channels)(*[float(v) for v in (np.linspace(-0.4, 0.4, channels) * 1.0e6)])
+            devs = (f * channels)(*([2.0e4] * channels))
+            rc = abi.lib.gsdrxStreamCreateMulti(ctypes.byref(h), kind, fmt, DECIM, taps.data_ptr(), TAPS, f(1.0e6),
+                                                f(0.0), ctypes.cast(chans, ctypes.c_void_p),
+                                                ctypes.cast(devs, ctypes.c_void_p), channels, 0, device.index)
         assert rc == 0, rc
-        cs = N_IN // chunks
         argsets = []
         for x in xs:
             for c in range(chunks):
@@ -660,11 +686,11 @@ def stream_rate(torch, abi, device, taps, xs, stream, t_call, kind, fmt, chunk_c
                 argsets.append((h, x.data_ptr() + sb * cs * c, n, yp, ycap, wref, stream))
         fn = abi.lib.gsdrxStreamProcess
         k = 0
-        for _ in range(max(20, 8 * chunks)):
+        for _ in range(max(20, min(8 * chunks, 2048))):
             assert fn(*argsets[k % len(argsets)]) == 0
             k += 1
         torch.cuda.synchronize()
-        calls = 50 * chunks
+        calls = max(50 * chunks, 200) if chunks <= 32 else max(2 * chunks, 256)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         h0 = time.perf_counter()
@@ -676,9 +702,15 @@ def stream_rate(torch, abi, device, taps, xs, stream, t_call, kind, fmt, chunk_c
         torch.cuda.synchronize()
         t = e0.elapsed_time(e1) / calls * chunks * 1e-3  # per channel pass
         abi.lib.gsdrxStreamDestroy(h)
-        res[f"{chunks}_chunks"] = {"us_per_channel": round(t * 1e6, 2), "msamples_per_s": round(N_IN / t / 1e6, 1),
-                                   "vs_single_call": round(t_call / t, 3),
-                                   "host_us_per_call": round((h1 - h0) / calls * 1e6, 2)}
+        res[name] = {"us_per_pass": round(t * 1e6, 2), "samples_per_call": cs, "calls_per_pass": chunks,
+                     "us_per_call": round(t * 1e6 / chunks, 3), "msamples_per_s": round(N_IN / t / 1e6, 1),
+                     "vs_single_call": round(channels * t_call / t, 3),
+                     "host_us_per_call": round((h1 - h0) / calls * 1e6, 2)}
+        if channels > 1:
+            res[name]["channel_msamples_per_s"] = round(channels * N_IN / t / 1e6, 1)
+    if channels > 1:
+        res["channels"] = channels
+        res["vs_single_call_def"] = "C x (one single-channel call over the whole channel) / (one pass of the C-channel stream)"
     return res
 
 

@@ -91,6 +91,7 @@ SIGNATURES = {
     "gsdrxAmDemodMulti": (_err, [_f, _f, _p, _u32, _u32, _sz, _p, _sz, _int, _p, _p, _sz, _i32, _p]),
     # stream.h
     "gsdrxStreamCreate": (_err, [ctypes.POINTER(_p), _int, _int, _u32, _p, _sz, _f, _f, _f, _f, _sz, _i32]),
+    "gsdrxStreamCreateMulti": (_err, [ctypes.POINTER(_p), _int, _int, _u32, _p, _sz, _f, _f, _p, _p, _u32, _sz, _i32]),
     "gsdrxStreamOutputsFor": (_sz, [_p, _sz]),
     "gsdrxStreamProcess": (_err, [_p, _p, _sz, _p, _sz, ctypes.POINTER(_sz), _p]),
     "gsdrxStreamDestroy": (_err, [_p]),

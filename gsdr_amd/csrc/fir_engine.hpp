@@ -1201,6 +1201,7 @@ struct MultiParams {
   uint32_t count;                     // channels in this launch
   uint32_t inc[kMaxMultiChannels];    // NCO phase increment per channel
   float gain[kMaxMultiChannels];      // FM gain per channel
+  uint64_t out_stride;                // outputs between consecutive channels' first outputs (>= N)
 };
 
 // Kernel 1g: multi-channel chains as C single-channel tiles per input tile, grouped for the L2. Block b
@@ -1220,7 +1221,8 @@ __global__ __launch_bounds__(WG) void k_fir_poly_grouped(FirParams p, MultiParam
   FirParams pc = p;
   pc.nco_inc = mp.inc[c];
   pc.fm_gain = mp.gain[c];
-  pc.out = reinterpret_cast<float*>(p.out) + (uint64_t)c * p.N;
+  pc.out = reinterpret_cast<float*>(p.out) + (uint64_t)c * mp.out_stride;
+  if (c != 0) pc.hist_out = nullptr;  // a multi-channel stream step: channel 0's workgroup 0 copies the history
   fir_poly_tile<TapT, InT, D, R, JC, WG, VEC, MODE, 0, true, 0, false, SH>(pc, tile);
 }
 

@@ -82,6 +82,7 @@ static hipError_t chain_multi_entry(int mode, float fs, float tune, const float*
     const uint32_t n = count - c0 < (uint32_t)kMaxMultiChannels ? count - c0 : (uint32_t)kMaxMultiChannels;
     MultiParams mp{};
     mp.count = n;
+    mp.out_stride = numOutputs;
     for (uint32_t c = 0; c < n; ++c) {
       if (!nco_increment(fs, tune, chans[c0 + c], &mp.inc[c])) return hipErrorInvalidValue;
       mp.gain[c] = mode == kModeFm ? fs / (2.0f * kPiF * devs[c0 + c]) : 0.0f;
@@ -192,6 +193,58 @@ hipError_t chain_stream_step_tiled(int mode, bool int8, float fs, float tune, fl
   }
   return mode == kModeFm ? stream_step_tiled<float2, kModeFm>(job, stream)
                          : stream_step_tiled<float2, kModeAm>(job, stream);
+}
+
+// The multi-channel streaming object's one-launch step (stream.hip, gsdrxStreamCreateMulti) on complex float
+// chunks: the grouped kernel of gsdrxFmDemodMulti / gsdrxAmDemodMulti (up to kMaxMultiChannels channels a
+// launch) with the single-channel stream step's operands -- output 0's window at chunk offset inOff, seam
+// samples read from the shared input history, the next history copied by workgroup 0 of the first launch.
+// Channel c's outputs go to output + c * outStride. Each workgroup runs the single-channel tile, so channel c
+// is bit-identical to its own gsdrxStream (and to one monolithic call). hipErrorNotSupported (nothing
+// launched): the shape has no grouped kernel; the stream then runs the channels one by one.
+hipError_t chain_multi_stream_step(int mode, float fs, float tune, const float* chans, const float* devs, uint32_t count,
+                                   uint32_t decimation, size_t firstSampleIndex, const float* taps, size_t tapCount,
+                                   const hipFloatComplex* chunk, uint64_t chunkLen, int64_t inOff,
+                                   const hipFloatComplex* hist, uint64_t histLen, hipFloatComplex* histOut,
+                                   int64_t histFrom, uint64_t histN, float* output, size_t outStride, size_t numOutputs,
+                                   int32_t device, hipStream_t stream) {
+  if (numOutputs == 0 || count == 0 || tapCount == 0 || taps == nullptr || tapCount > (1u << 26)) {
+    return hipErrorNotSupported;
+  }
+  if (decimation != 2 && decimation != 4 && decimation != 8) return hipErrorNotSupported;
+  DeviceScope scope(device);
+  if (scope.status() != hipSuccess) return scope.status();
+  for (uint32_t c0 = 0; c0 < count; c0 += kMaxMultiChannels) {
+    const uint32_t n = count - c0 < (uint32_t)kMaxMultiChannels ? count - c0 : (uint32_t)kMaxMultiChannels;
+    MultiParams mp{};
+    mp.count = n;
+    mp.out_stride = outStride;
+    for (uint32_t c = 0; c < n; ++c) {
+      if (!nco_increment(fs, tune, chans[c0 + c], &mp.inc[c])) return hipErrorInvalidValue;
+      mp.gain[c] = mode == kModeFm ? fs / (2.0f * kPiF * devs[c0 + c]) : 0.0f;
+    }
+    FirJob job;
+    job.in = reinterpret_cast<const float2*>(chunk) + inOff;  // output 0's window (may precede the chunk)
+    job.L = (uint64_t)((int64_t)chunkLen - inOff);
+    job.taps = taps;
+    job.out = output + (size_t)c0 * outStride;
+    job.D = decimation;
+    job.T = tapCount;
+    job.N = numOutputs;
+    job.mode = mode;
+    job.nco_n0 = (uint32_t)firstSampleIndex;
+    job.in_off = inOff;
+    job.hist = hist;
+    job.hist_len = histLen;
+    job.hist_out = c0 == 0 ? histOut : nullptr;  // every group reads the old history; the first writes the next
+    job.hist_from = histFrom;
+    job.hist_n = histN;
+    job.stream_tiled = true;
+    const hipError_t e = mode == kModeFm ? launch_multi_chain<float2, kModeFm>(job, mp, stream)
+                                         : launch_multi_chain<float2, kModeAm>(job, mp, stream);
+    if (e != hipSuccess) return e;  // hipErrorNotSupported only from the first group (same shape for all)
+  }
+  return hipSuccess;
 }
 
 }  // namespace gsdr

@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <new>
+#include <vector>
 
 #include "gsdr/am.h"
 #include "gsdr/fir.h"
@@ -31,7 +32,7 @@ struct gsdrxStream_t {
   const float* taps = nullptr;
   size_t T = 0;
   size_t W = 0;  // samples one output needs
-  float fs = 0.0f, tune = 0.0f, chan = 0.0f, dev = 0.0f;
+  float fs = 0.0f, tune = 0.0f;
   uint64_t n0 = 0;  // absolute index of stream sample 0
   int32_t device = 0;
   size_t sb = 8;  // bytes per input sample
@@ -41,6 +42,9 @@ struct gsdrxStream_t {
   char* hist = nullptr;   // samples [next_out * D, consumed) (empty if next_out * D >= consumed)
   char* spare = nullptr;  // the other history buffer (ping-pong)
   char* seam = nullptr;   // history + chunk head for the seam outputs
+  // channels of one RF input (gsdrxStreamCreateMulti; one channel for gsdrxStreamCreate): frequency and
+  // deviation per channel, channel c's outputs at output + c * outputCapacity
+  std::vector<float> chans, devs;
 };
 
 namespace gsdr {
@@ -66,6 +70,12 @@ hipError_t chain_stream_step_tiled(int mode, bool int8, float fs, float tune, fl
                                    uint64_t chunkLen, int64_t inOff, const void* hist, uint64_t histLen, void* histOut,
                                    int64_t histFrom, uint64_t histN, float* output, size_t numOutputs, int32_t device,
                                    hipStream_t stream);
+hipError_t chain_multi_stream_step(int mode, float fs, float tune, const float* chans, const float* devs, uint32_t count,
+                                   uint32_t decimation, size_t firstSampleIndex, const float* taps, size_t tapCount,
+                                   const hipFloatComplex* chunk, uint64_t chunkLen, int64_t inOff,
+                                   const hipFloatComplex* hist, uint64_t histLen, hipFloatComplex* histOut,
+                                   int64_t histFrom, uint64_t histN, float* output, size_t outStride, size_t numOutputs,
+                                   int32_t device, hipStream_t stream);
 // fm_am.hip (mode 1 = FM, 2 = AM as in fir_engine.hpp)
 hipError_t chain_int8_stream_step(int mode, float fs, float tune, float chan, float dev, size_t firstSampleIndex,
                                   const float* taps, size_t tapCount, const int8_t* chunk, uint64_t chunkLen,
@@ -96,8 +106,10 @@ Plan make_plan(uint32_t D, uint64_t W, uint64_t S, uint64_t m_next, uint64_t M) 
   return p;
 }
 
-hipError_t filter(const gsdrxStream_t& s, const void* in, uint64_t first, void* out, size_t n, hipStream_t st) {
+hipError_t filter(const gsdrxStream_t& s, size_t c, const void* in, uint64_t first, void* out, size_t n,
+                  hipStream_t st) {
   const bool i8 = s.format == GSDRX_SAMPLES_CS8;
+  const float chan = s.chans[c], dev = s.devs[c];
   switch (s.kind) {
     case GSDRX_STREAM_FIR:
       // the default path of gsdrxFirFCInt8 told the output's absolute index: the decimation-4 matrix-core
@@ -107,14 +119,14 @@ hipError_t filter(const gsdrxStream_t& s, const void* in, uint64_t first, void* 
                 : gsdrFirFC(s.D, s.taps, s.T, static_cast<const hipFloatComplex*>(in),
                             static_cast<hipFloatComplex*>(out), n, s.device, st);
     case GSDRX_STREAM_FM:
-      return i8 ? gsdrxFmDemodInt8(s.fs, s.tune, s.chan, s.dev, s.D, first, s.taps, s.T,
+      return i8 ? gsdrxFmDemodInt8(s.fs, s.tune, chan, dev, s.D, first, s.taps, s.T,
                                    static_cast<const int8_t*>(in), static_cast<float*>(out), n, s.device, st)
-                : gsdrFmDemod(s.fs, s.tune, s.chan, s.dev, s.D, first, s.taps, s.T,
+                : gsdrFmDemod(s.fs, s.tune, chan, dev, s.D, first, s.taps, s.T,
                               static_cast<const hipFloatComplex*>(in), static_cast<float*>(out), n, s.device, st);
     default:
-      return i8 ? gsdrxAmDemodInt8(s.fs, s.tune, s.chan, s.D, first, s.taps, s.T,
+      return i8 ? gsdrxAmDemodInt8(s.fs, s.tune, chan, s.D, first, s.taps, s.T,
                                    static_cast<const int8_t*>(in), static_cast<float*>(out), n, s.device, st)
-                : gsdrAmDemod(s.fs, s.tune, s.chan, s.D, first, s.taps, s.T, static_cast<const hipFloatComplex*>(in),
+                : gsdrAmDemod(s.fs, s.tune, chan, s.D, first, s.taps, s.T, static_cast<const hipFloatComplex*>(in),
                               static_cast<float*>(out), n, s.device, st);
   }
 }
@@ -181,13 +193,14 @@ GSDR_C_LINKAGE void gsdrxStreamPlan(uint32_t decimation, size_t window, uint64_t
   plan[4] = p.hist_after;
 }
 
-GSDR_C_LINKAGE hipError_t gsdrxStreamCreate(gsdrxStream* stream, int kind, int sampleFormat, uint32_t decimation,
-                                            const float* taps, size_t tapCount, float rfSampleRate,
-                                            float tuningFrequency, float channelFrequency, float frequencyDeviation,
-                                            size_t firstSampleIndex, int32_t cudaDevice) GSDR_NO_EXCEPT {
+namespace gsdr {
+namespace {
+hipError_t create_stream(gsdrxStream* stream, int kind, int sampleFormat, uint32_t decimation, const float* taps,
+                         size_t tapCount, float rfSampleRate, float tuningFrequency, const float* chans,
+                         const float* devs, uint32_t count, size_t firstSampleIndex, int32_t cudaDevice) {
   if (stream == nullptr) return hipErrorInvalidValue;
   *stream = nullptr;
-  if (decimation == 0 || tapCount == 0 || taps == nullptr) return hipErrorInvalidValue;
+  if (decimation == 0 || tapCount == 0 || taps == nullptr || count == 0) return hipErrorInvalidValue;
   if (kind != GSDRX_STREAM_FIR && kind != GSDRX_STREAM_FM && kind != GSDRX_STREAM_AM) return hipErrorInvalidValue;
   if (sampleFormat != GSDRX_SAMPLES_CF32 && sampleFormat != GSDRX_SAMPLES_CS8) return hipErrorInvalidValue;
   gsdrxStream s = new (std::nothrow) gsdrxStream_t;
@@ -200,13 +213,18 @@ GSDR_C_LINKAGE hipError_t gsdrxStreamCreate(gsdrxStream* stream, int kind, int s
   s->W = kind == GSDRX_STREAM_FM ? tapCount + decimation : tapCount;
   s->fs = rfSampleRate;
   s->tune = tuningFrequency;
-  s->chan = channelFrequency;
-  s->dev = frequencyDeviation;
+  try {
+    s->chans.assign(chans, chans + count);
+    s->devs.assign(devs, devs + count);
+  } catch (...) {
+    delete s;
+    return hipErrorOutOfMemory;
+  }
   s->n0 = firstSampleIndex;
   s->device = cudaDevice;
   s->sb = sampleFormat == GSDRX_SAMPLES_CS8 ? 2 : 8;
   s->ob = kind == GSDRX_STREAM_FIR ? 8 : 4;
-  gsdr::DeviceScope scope(cudaDevice);
+  DeviceScope scope(cudaDevice);
   hipError_t e = scope.status();
   const size_t hist_bytes = s->W * s->sb;  // history < W samples
   const size_t seam_bytes = 2 * s->W * s->sb;
@@ -219,6 +237,38 @@ GSDR_C_LINKAGE hipError_t gsdrxStreamCreate(gsdrxStream* stream, int kind, int s
   }
   *stream = s;
   return hipSuccess;
+}
+}  // namespace
+}  // namespace gsdr
+
+GSDR_C_LINKAGE hipError_t gsdrxStreamCreate(gsdrxStream* stream, int kind, int sampleFormat, uint32_t decimation,
+                                            const float* taps, size_t tapCount, float rfSampleRate,
+                                            float tuningFrequency, float channelFrequency, float frequencyDeviation,
+                                            size_t firstSampleIndex, int32_t cudaDevice) GSDR_NO_EXCEPT {
+  return gsdr::create_stream(stream, kind, sampleFormat, decimation, taps, tapCount, rfSampleRate, tuningFrequency,
+                             &channelFrequency, &frequencyDeviation, 1, firstSampleIndex, cudaDevice);
+}
+
+GSDR_C_LINKAGE hipError_t gsdrxStreamCreateMulti(gsdrxStream* stream, int kind, int sampleFormat, uint32_t decimation,
+                                                 const float* taps, size_t tapCount, float rfSampleRate,
+                                                 float tuningFrequency, const float* channelFrequencies,
+                                                 const float* frequencyDeviations, uint32_t numChannels,
+                                                 size_t firstSampleIndex, int32_t cudaDevice) GSDR_NO_EXCEPT {
+  if (stream != nullptr) *stream = nullptr;
+  if (kind != GSDRX_STREAM_FM && kind != GSDRX_STREAM_AM) return hipErrorInvalidValue;
+  if (numChannels == 0 || channelFrequencies == nullptr) return hipErrorInvalidValue;
+  if (kind == GSDRX_STREAM_FM && frequencyDeviations == nullptr) return hipErrorInvalidValue;
+  std::vector<float> ones;
+  if (frequencyDeviations == nullptr) {  // AM: deviations unused
+    try {
+      ones.assign(numChannels, 1.0f);
+    } catch (...) {
+      return hipErrorOutOfMemory;
+    }
+    frequencyDeviations = ones.data();
+  }
+  return gsdr::create_stream(stream, kind, sampleFormat, decimation, taps, tapCount, rfSampleRate, tuningFrequency,
+                             channelFrequencies, frequencyDeviations, numChannels, firstSampleIndex, cudaDevice);
 }
 
 GSDR_C_LINKAGE size_t gsdrxStreamOutputsFor(gsdrxStream s, size_t numInputSamples) GSDR_NO_EXCEPT {
@@ -241,47 +291,70 @@ GSDR_C_LINKAGE hipError_t gsdrxStreamProcess(gsdrxStream s, const void* input, s
   if (scope.status() != hipSuccess) return scope.status();
   const char* chunk = static_cast<const char*>(input);
   char* out = static_cast<char*>(output);
+  const size_t C = s->chans.size();
+  const size_t ostride = outputCapacity * s->ob;  // bytes between channels' output blocks
   const uint64_t S = s->consumed, h0 = s->next_out * s->D;
   const uint64_t h = S > h0 ? S - h0 : 0;
   hipError_t e = hipSuccess;
   if (n_out > 0) {
-    // ONE launch does the seam outputs (their samples before the chunk read from the history buffer), the
-    // direct outputs and the next history copy: the int8 matrix-core kernels at decimation 4, the tiled
-    // kernels otherwise (the same kernels as one monolithic call, tile for tile)
+    // ONE launch (per channel, or per 16 channels on the grouped kernel) does the seam outputs (their samples
+    // before the chunk read from the history buffer), the direct outputs and the next history copy: the int8
+    // matrix-core kernels at decimation 4, the tiled kernels otherwise (the same kernels as one monolithic
+    // call, tile for tile). Every channel reads the old history; only channel 0's launch writes the next one.
     const int64_t in_off = (int64_t)(s->next_out * s->D) - (int64_t)S;
     const int64_t from = (int64_t)(p.m_end * s->D) - (int64_t)S;
     const bool i8 = s->format == GSDRX_SAMPLES_CS8;
     const int mode = s->kind == GSDRX_STREAM_FM ? 1 : 2;
     e = hipErrorNotSupported;
-    if (i8 && s->D == 4) {
-      const int8_t* c8 = reinterpret_cast<const int8_t*>(chunk);
-      const int8_t* h8 = reinterpret_cast<const int8_t*>(s->hist);
-      int8_t* n8 = reinterpret_cast<int8_t*>(s->spare);
-      if (s->kind == GSDRX_STREAM_FIR) {
-        e = gsdr::fir_int8_stream_step(s->next_out, s->taps, s->T, c8, numInputSamples, in_off, h8, h, n8, from,
-                                       p.hist_after, reinterpret_cast<hipFloatComplex*>(out), n_out, s->device,
-                                       cudaStream);
-      } else {
-        e = gsdr::chain_int8_stream_step(mode, s->fs, s->tune, s->chan, s->dev, s->n0 + h0, s->taps, s->T, c8,
-                                         numInputSamples, in_off, h8, h, n8, from, p.hist_after,
-                                         reinterpret_cast<float*>(out), n_out, s->device, cudaStream);
-      }
+    if (C > 1 && !i8) {
+      e = gsdr::chain_multi_stream_step(mode, s->fs, s->tune, s->chans.data(), s->devs.data(), (uint32_t)C, s->D,
+                                        s->n0 + h0, s->taps, s->T, reinterpret_cast<const hipFloatComplex*>(chunk),
+                                        numInputSamples, in_off, reinterpret_cast<const hipFloatComplex*>(s->hist), h,
+                                        reinterpret_cast<hipFloatComplex*>(s->spare), from, p.hist_after,
+                                        reinterpret_cast<float*>(out), outputCapacity, n_out, s->device, cudaStream);
     }
-    if (e == hipErrorNotSupported) {
-      if (s->kind == GSDRX_STREAM_FIR) {
-        e = i8 ? gsdr::fir_int8_stream_step_tiled(s->D, s->taps, s->T, reinterpret_cast<const int8_t*>(chunk),
-                                                  numInputSamples, in_off, reinterpret_cast<const int8_t*>(s->hist), h,
-                                                  reinterpret_cast<int8_t*>(s->spare), from, p.hist_after,
-                                                  reinterpret_cast<hipFloatComplex*>(out), n_out, s->device, cudaStream)
-               : gsdr::fir_fc_stream_step(s->D, s->taps, s->T, reinterpret_cast<const hipFloatComplex*>(chunk),
-                                          numInputSamples, in_off, reinterpret_cast<const hipFloatComplex*>(s->hist), h,
-                                          reinterpret_cast<hipFloatComplex*>(s->spare), from, p.hist_after,
-                                          reinterpret_cast<hipFloatComplex*>(out), n_out, s->device, cudaStream);
-      } else {
-        e = gsdr::chain_stream_step_tiled(mode, i8, s->fs, s->tune, s->chan, s->dev, s->D, s->n0 + h0, s->taps, s->T,
-                                          chunk, numInputSamples, in_off, s->hist, h, s->spare, from, p.hist_after,
-                                          reinterpret_cast<float*>(out), n_out, s->device, cudaStream);
+    // otherwise one launch per channel; a shape without a one-launch step returns hipErrorNotSupported from
+    // channel 0, before anything was launched, and the call takes the seam path below
+    for (size_t c = 0; c < C && e == hipErrorNotSupported; ++c) {
+      void* hout = c == 0 ? s->spare : nullptr;
+      char* oc = out + c * ostride;
+      hipError_t ec = hipErrorNotSupported;
+      if (i8 && s->D == 4) {
+        const int8_t* c8 = reinterpret_cast<const int8_t*>(chunk);
+        const int8_t* h8 = reinterpret_cast<const int8_t*>(s->hist);
+        int8_t* n8 = static_cast<int8_t*>(hout);
+        if (s->kind == GSDRX_STREAM_FIR) {
+          ec = gsdr::fir_int8_stream_step(s->next_out, s->taps, s->T, c8, numInputSamples, in_off, h8, h, n8, from,
+                                          p.hist_after, reinterpret_cast<hipFloatComplex*>(oc), n_out, s->device,
+                                          cudaStream);
+        } else {
+          ec = gsdr::chain_int8_stream_step(mode, s->fs, s->tune, s->chans[c], s->devs[c], s->n0 + h0, s->taps, s->T,
+                                            c8, numInputSamples, in_off, h8, h, n8, from, p.hist_after,
+                                            reinterpret_cast<float*>(oc), n_out, s->device, cudaStream);
+        }
       }
+      if (ec == hipErrorNotSupported) {
+        if (s->kind == GSDRX_STREAM_FIR) {
+          ec = i8 ? gsdr::fir_int8_stream_step_tiled(s->D, s->taps, s->T, reinterpret_cast<const int8_t*>(chunk),
+                                                     numInputSamples, in_off, reinterpret_cast<const int8_t*>(s->hist), h,
+                                                     static_cast<int8_t*>(hout), from, p.hist_after,
+                                                     reinterpret_cast<hipFloatComplex*>(oc), n_out, s->device, cudaStream)
+                  : gsdr::fir_fc_stream_step(s->D, s->taps, s->T, reinterpret_cast<const hipFloatComplex*>(chunk),
+                                             numInputSamples, in_off, reinterpret_cast<const hipFloatComplex*>(s->hist), h,
+                                             static_cast<hipFloatComplex*>(hout), from, p.hist_after,
+                                             reinterpret_cast<hipFloatComplex*>(oc), n_out, s->device, cudaStream);
+        } else {
+          ec = gsdr::chain_stream_step_tiled(mode, i8, s->fs, s->tune, s->chans[c], s->devs[c], s->D, s->n0 + h0,
+                                             s->taps, s->T, chunk, numInputSamples, in_off, s->hist, h, hout, from,
+                                             p.hist_after, reinterpret_cast<float*>(oc), n_out, s->device, cudaStream);
+        }
+      }
+      if (ec == hipErrorNotSupported && c == 0) break;
+      if (ec != hipSuccess) {
+        e = ec == hipErrorNotSupported ? hipErrorUnknown : ec;  // (one shape for every channel: cannot happen)
+        break;
+      }
+      if (c + 1 == C) e = hipSuccess;
     }
     if (e == hipSuccess) {
       std::swap(s->hist, s->spare);
@@ -310,10 +383,13 @@ GSDR_C_LINKAGE hipError_t gsdrxStreamProcess(gsdrxStream s, const void* input, s
     g.add(s->spare + done * s->sb, chunk + c0 * s->sb, (S_new - S - c0) * s->sb);
   }
   e = gsdr::gather(g, cudaStream);
-  if (e == hipSuccess && p.n_seam) e = gsdr::filter(*s, s->seam, s->n0 + h0, out, p.n_seam, cudaStream);
-  if (e == hipSuccess && p.n_main) {
-    e = gsdr::filter(*s, chunk + p.main_off * s->sb, s->n0 + p.m_mid * s->D, out + p.n_seam * s->ob, p.n_main,
-                     cudaStream);
+  for (size_t c = 0; c < C && e == hipSuccess; ++c) {
+    char* oc = out + c * ostride;
+    if (p.n_seam) e = gsdr::filter(*s, c, s->seam, s->n0 + h0, oc, p.n_seam, cudaStream);
+    if (e == hipSuccess && p.n_main) {
+      e = gsdr::filter(*s, c, chunk + p.main_off * s->sb, s->n0 + p.m_mid * s->D, oc + p.n_seam * s->ob, p.n_main,
+                       cudaStream);
+    }
   }
   if (e == hipSuccess && p.hist_after) std::swap(s->hist, s->spare);
   if (e != hipSuccess) return e;

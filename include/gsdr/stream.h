@@ -70,12 +70,43 @@ GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxStreamCreate(
     size_t firstSampleIndex,
     int32_t cudaDevice) GSDR_NO_EXCEPT;
 
-/** Number of outputs the next gsdrxStreamProcess call with `numInputSamples` samples will write. */
+/**
+ * Create a MULTI-CHANNEL stream: `numChannels` FM or AM channels of one RF input (the streaming form of
+ * gsdrxFmDemodMulti / gsdrxAmDemodMulti; the intent of the reference's dead k_Fm4x, src/fm.cu:71-179).
+ * Channel c mixes by tuningFrequency - channelFrequencies[c] and, for FM, uses frequencyDeviations[c]
+ * (ignored, and may be null, for AM). The input history is kept once for all channels. Each
+ * gsdrxStreamProcess call is one launch per 16 channels for complex float input at decimation 2, 4 or 8
+ * (the grouped kernel: each input tile read from HBM about once for all its channels), one launch per channel
+ * otherwise (int8 I/Q at decimation 4: the matrix-core chain of each channel). Channel c's outputs are
+ * bit-identical to a single-channel gsdrxStream with that channel's frequency (and so to one monolithic
+ * gsdrFmDemod / gsdrAmDemod / gsdrx*Int8 call). In gsdrxStreamProcess, channel c's outputs go to
+ * output + c * outputCapacity (outputCapacity = the per-channel capacity, in outputs), and
+ * *numOutputsWritten / gsdrxStreamOutputsFor count the outputs of ONE channel.
+ * Returns hipErrorInvalidValue for kind GSDRX_STREAM_FIR, numChannels == 0, null channelFrequencies, null
+ * frequencyDeviations for FM, and as gsdrxStreamCreate.
+ */
+GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxStreamCreateMulti(
+    gsdrxStream* stream,
+    int kind,
+    int sampleFormat,
+    uint32_t decimation,
+    const float* taps,
+    size_t tapCount,
+    float rfSampleRate,
+    float tuningFrequency,
+    const float* channelFrequencies,
+    const float* frequencyDeviations,
+    uint32_t numChannels,
+    size_t firstSampleIndex,
+    int32_t cudaDevice) GSDR_NO_EXCEPT;
+
+/** Number of outputs (per channel) the next gsdrxStreamProcess call with `numInputSamples` samples will write. */
 GSDR_C_LINKAGE GSDR_PUBLIC size_t gsdrxStreamOutputsFor(gsdrxStream stream, size_t numInputSamples) GSDR_NO_EXCEPT;
 
 /**
  * Append `numInputSamples` samples (device memory, in the stream's sample format) and write every
- * output that became computable to `output` (hipFloatComplex for FIR, float for FM/AM), in order.
+ * output that became computable to `output` (hipFloatComplex for FIR, float for FM/AM), in order
+ * (a multi-channel stream: channel c's at output + c * outputCapacity).
  * `*numOutputsWritten` receives the count (host-known, no synchronisation). Asynchronous on
  * `cudaStream`; the input chunk may be reused once the stream's work has completed. Returns
  * hipErrorInvalidValue, leaving the stream unchanged, when outputCapacity is too small.

@@ -127,3 +127,96 @@ def test_create_validation(cuda):
     assert abi.lib.gsdrxStreamCreate(ctypes.byref(h), 7, 0, 2, taps.data_ptr(), 4, 1.0, 0.0, 0.0, 1.0, 0, 0) != 0
     assert abi.lib.gsdrxStreamCreate(ctypes.byref(h), 0, 0, 2, None, 4, 1.0, 0.0, 0.0, 1.0, 0, 0) != 0
     assert abi.lib.gsdrxStreamDestroy(None) == 0
+
+
+# Multi-channel streams (gsdrxStreamCreateMulti, SURVEY.md 8(f) rows 1 x 3): C channels of one RF input, one
+# shared history; channel c must equal its own single-channel stream and one monolithic call, bit for bit.
+MCH = [1.0e5, -2.5e5, 3.3e4, 0.0, -4.4e5, 1.7e5, 2.9e5, -1.1e5, 4.0e5, -3.0e5, 6.0e4, -6.0e4, 2.2e5, -2.2e5, 1.3e5,
+       -1.3e5, 3.7e5, -3.7e5, 9.0e3]
+
+
+@pytest.mark.parametrize("kind", ["fm", "am"])
+@pytest.mark.parametrize("int8", [False, True])
+@pytest.mark.parametrize("D,C", [(4, 3), (4, 17), (2, 5), (8, 2), (3, 4), (9, 3)])
+def test_multi_stream_equals_single_streams(cuda, kind, int8, D, C):
+    """D = 2 / 4 / 8 complex float: the grouped kernel (17 channels: two launches a call, the second without the
+    history copy); int8 at D = 4: per-channel matrix-core chains; D = 3: per-channel tiled steps; D = 9: the
+    shared seam plan (one gather, then each channel's two filter calls)."""
+    from gsdr_amd.signals import fm_test_signal, lowpass_taps
+    from gsdr_amd.stream import Stream
+
+    T, n0 = 127, 4_000_000_123
+    L = 120_000 + 7 * D
+    x = fm_test_signal(L, noise=0.02, n0=n0)
+    if int8:
+        xh = np.clip(np.round(np.stack([x.real, x.imag], 1).ravel() * 100), -128, 127).astype(np.int8)
+        per = 2
+    else:
+        xh, per = x, 1
+    xd = torch.from_numpy(xh).to(cuda)
+    taps = torch.from_numpy(lowpass_taps(T)).to(cuda)
+    chans = MCH[:C]
+    devs = [DEV * (1 + 0.1 * c) for c in range(C)]
+    ms = Stream(kind, taps, D, FS, TUNE, chans, devs, first_sample_index=n0, int8=int8)
+    W = T + D if kind == "fm" else T
+    parts, pos = [], 0
+    sizes = chunks(L, seed=D * 100 + C + int8, W=W)
+    for m in sizes:
+        parts.append(ms.process(xd[pos * per:(pos + m) * per]).clone())
+        pos += m
+    ms.close()
+    got = torch.cat(parts, dim=1)
+    torch.cuda.synchronize()
+    for c in range(C):
+        s = Stream(kind, taps, D, FS, TUNE, chans[c], devs[c], first_sample_index=n0, int8=int8)
+        single, pos = [], 0
+        for m in sizes:
+            single.append(s.process(xd[pos * per:(pos + m) * per]).clone())
+            pos += m
+        s.close()
+        want = torch.cat(single)
+        assert got.shape[1] == want.numel(), (c, got.shape, want.numel())
+        assert torch.equal(got[c].view(torch.int32), want.view(torch.int32)), c
+    # and the first and last channels against one monolithic call
+    from gsdr_amd import ops
+
+    for c in (0, C - 1):
+        if kind == "fm":
+            mono = ops.fm_demod(xd, taps, FS, TUNE, chans[c], devs[c], D, n0)
+        else:
+            mono = ops.am_demod(xd, taps, FS, TUNE, chans[c], D, n0)
+        assert torch.equal(got[c].view(torch.int32), mono.view(torch.int32)), c
+
+
+def test_multi_stream_output_stride_and_validation(cuda):
+    """Channel c's outputs land at output + c * outputCapacity (a caller's fixed per-channel buffers), the rest of
+    each row untouched; FIR kind, zero channels and a null deviation list for FM are refused."""
+    import ctypes
+
+    from gsdr_amd.abi import lib
+    from gsdr_amd.signals import fm_test_signal, lowpass_taps
+    from gsdr_amd.stream import Stream
+
+    T, D = 63, 4
+    taps = torch.from_numpy(lowpass_taps(T)).to(cuda)
+    x = torch.from_numpy(fm_test_signal(50_000, noise=0.02)).to(cuda)
+    s = Stream("fm", taps, D, FS, TUNE, [1e5, -1e5, 2e5], [DEV] * 3)
+    cap = 20_000
+    out = torch.full((3, cap), 7.0, device=cuda)
+    y = s.process(x, out=out)
+    n = y.shape[1]
+    assert n == (50_000 - T - D) // D + 1 and n < cap
+    assert torch.all(out[:, n:] == 7.0)
+    for c, f in enumerate([1e5, -1e5, 2e5]):
+        from gsdr_amd import ops
+
+        assert torch.equal(out[c, :n], ops.fm_demod(x, taps, FS, TUNE, f, DEV, D, 0, n))
+    s.close()
+    h = ctypes.c_void_p()
+    f2 = (ctypes.c_float * 2)(1e5, 2e5)
+    p = ctypes.cast(f2, ctypes.c_void_p)
+    assert lib.gsdrxStreamCreateMulti(ctypes.byref(h), 0, 0, 4, taps.data_ptr(), T, FS, 0.0, p, p, 2, 0, 0) != 0
+    assert lib.gsdrxStreamCreateMulti(ctypes.byref(h), 1, 0, 4, taps.data_ptr(), T, FS, 0.0, p, p, 0, 0, 0) != 0
+    assert lib.gsdrxStreamCreateMulti(ctypes.byref(h), 1, 0, 4, taps.data_ptr(), T, FS, 0.0, p, None, 2, 0, 0) != 0
+    assert lib.gsdrxStreamCreateMulti(ctypes.byref(h), 2, 0, 4, taps.data_ptr(), T, FS, 0.0, p, None, 2, 0, 0) == 0
+    assert lib.gsdrxStreamDestroy(h) == 0

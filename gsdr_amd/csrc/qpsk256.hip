@@ -25,6 +25,7 @@
 #include <algorithm>
 #include <cmath>
 #include <map>
+#include <type_traits>
 #include <vector>
 
 #include "awgn.hpp"
@@ -203,6 +204,23 @@ __device__ __forceinline__ uint32_t demod_rect_fast(const float* __restrict__ lx
   return demod_rect_tie(cx.d[0], cx.d[1], cx.d[2], cy.d[0], cy.d[1], cy.d[2], i0, q0);
 }
 
+// Rectangular decision in ~15 VALU operations, taken when it is provably the reference's answer. u is the symbol's
+// position in level units per axis (level k at u = k up to rounding: < 2^-17 of a level spacing, from scale, the
+// fma and the host-built levels). When the clamped u of both axes is more than kRectMargin from every midpoint
+// between two levels, the nearest level is unambiguous by a margin (in squared distance the runner-up is farther by
+// >= 2^-11 of dmin) that no rounding of the reference's cuCabsf ranking can reverse, so (i, q) is its first argmin.
+// Symbols within the margin of a midpoint (~1e-4 of noisy symbols) or beyond |re|,|im| <= 4|a| (or NaN) return
+// false and take demod_rect_fast's careful path.
+constexpr float kRectMargin = 0x1p-10f;
+__device__ __forceinline__ bool demod_rect_quick(float2 r, float lim, float scale, uint32_t& k) {
+  const gsdr_f32x2 u = __builtin_elementwise_fma(gsdr_f32x2{r.x, r.y}, gsdr_f32x2{scale, scale}, gsdr_f32x2{7.5f, 7.5f});
+  const float tx = __builtin_amdgcn_fmed3f(u.x, 0.0f, 15.0f), ty = __builtin_amdgcn_fmed3f(u.y, 0.0f, 15.0f);
+  const float ix = __builtin_rintf(tx), iy = __builtin_rintf(ty);
+  const gsdr_f32x2 d = gsdr_f32x2{tx, ty} - gsdr_f32x2{ix, iy};
+  k = (uint32_t)ix * 16u + (uint32_t)iy;
+  return fabsf(r.x) <= lim && fabsf(r.y) <= lim && fmaxf(fabsf(d.x), fabsf(d.y)) <= 0.5f - kRectMargin;
+}
+
 __device__ __forceinline__ void load_table(float2* lds_tab, uint32_t type) {
   const float2* src = c_qpsk256_tables[type == 0 ? 0 : 1];
   for (uint32_t i = threadIdx.x; i < 256; i += kCBlock) lds_tab[i] = src[i];
@@ -275,15 +293,31 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <int R3>
+// RECT (GSDR_C256_RECT_LEVELS = 1, a timing switch, off by default): the rectangular table's entry 16 i + q is
+// (lx[i], ly[q]) (qpsk256.cu:33-34), so a symbol's point can be two 4-byte reads from 16-entry level arrays --
+// conflict-free (distinct levels sit in distinct banks, equal ones broadcast) where the gather from the 256-entry
+// table puts up to ~4 lanes of a group on one bank. Measured side by side (profiles/r05_ab_config5.txt): 29.8 us
+// against 28.8 us for the gather. The kernel is VALU-bound (Philox), and the level reads cost ~17 more VALU
+// instructions per lane step (index splits, two address computations) than the bank conflicts cost in LDS time.
+// firstBlk = firstSymbolIndex / 3: with every lane's first symbol a multiple of 6 from the launch's first, its
+// first Philox block is firstBlk + s / 3 (no 64-bit division per lane).
+#ifndef GSDR_C256_RECT_LEVELS
+#define GSDR_C256_RECT_LEVELS 0
+#endif
+template <int R3, bool RECT>
 __global__ __launch_bounds__(kCBlock) void k_c256_mod_awgn(const uint8_t* __restrict__ in, float2* __restrict__ out,
                                                             uint32_t n, uint32_t type, float sigma, uint64_t seed,
-                                                            uint64_t first) {
+                                                            uint64_t firstBlk) {
   __shared__ float2 tab[256];
+  __shared__ float lev[32];  // RECT: lx[0..15], ly[0..15]
   __shared__ AwgnLds ntab;
   __shared__ float4 stage[kCBlock / 64][kAwgnWaveSyms / 2];  // per wave: 384 symbols as 192 float4
   awgn_load_table(ntab, kCBlock);
-  load_table(tab, type);  // its barrier publishes both tables
+  if constexpr (RECT) {
+    const float2* src = c_qpsk256_tables[0];
+    if (threadIdx.x < 32) lev[threadIdx.x] = threadIdx.x < 16 ? src[threadIdx.x * 16].x : src[threadIdx.x - 16].y;
+  }
+  load_table(tab, type);  // its barrier publishes the tables
   constexpr int NB = R3 == 0 ? 2 : 3;  // Philox blocks touched by six symbols starting at slot R3
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   float4* __restrict__ st = stage[wv];
@@ -298,7 +332,10 @@ __global__ __launch_bounds__(kCBlock) void k_c256_mod_awgn(const uint8_t* __rest
     if (ws >= n) break;
     const uint64_t s = ws + (uint64_t)kAwgnSym * lane;  // this lane's first symbol (a multiple of 6)
     const bool whole = ws + kAwgnWaveSyms <= n;          // wave-uniform
-    const uint64_t b0 = (first + s) / 3u;  // (first + s) % 3 == R3
+    // (first + s) / 3 with s = base + 384 (it * waves + wv) + 6 lane, every term a multiple of 3
+    const uint32_t s3 = (uint32_t)blockIdx.x * (kAwgnBlockSyms / 3u) + (kAwgnWaveSyms / 3u) * ((uint32_t)it * (kCBlock / 64) + wv) +
+                        2u * lane;
+    const uint64_t b0 = firstBlk + s3;
     // the main-table normals and outputs of the lane's six symbols
     auto load_syms = [&](uint8_t (&sym)[kAwgnSym]) {
       if (whole && in_even) {  // three 2-byte loads (s is even)
@@ -324,7 +361,7 @@ __global__ __launch_bounds__(kCBlock) void k_c256_mod_awgn(const uint8_t* __rest
 #pragma unroll
       for (int j = 0; j < kAwgnSym; ++j) {
         const float2 g = awgn_slot_main(ntab, w[(R3 + j) / 3], (R3 + j) % 3);
-        const float2 p = tab[sym[j]];
+        const float2 p = RECT ? make_float2(lev[sym[j] >> 4], lev[16 + (sym[j] & 15)]) : tab[sym[j]];
         y[j] = make_float2(p.x + sigma * g.x, p.y + sigma * g.y);
       }
     }
@@ -339,7 +376,7 @@ __global__ __launch_bounds__(kCBlock) void k_c256_mod_awgn(const uint8_t* __rest
 #pragma unroll
       for (int j = 0; j < kAwgnSym; ++j) {
         const float2 g = awgn_slot(ntab, w[(R3 + j) / 3], (R3 + j) % 3, seed, b0 + (R3 + j) / 3);
-        const float2 p = tab[sym[j]];
+        const float2 p = RECT ? make_float2(lev[sym[j] >> 4], lev[16 + (sym[j] & 15)]) : tab[sym[j]];
         y[j] = make_float2(p.x + sigma * g.x, p.y + sigma * g.y);
       }
     }
@@ -417,7 +454,9 @@ __global__ __launch_bounds__(kCBlock) void k_c256_demod(C256Streams st, uint32_t
   }
   auto demod = [&](float2 r) -> uint32_t {
     if constexpr (TYPE == 0) {
-      const uint32_t k = demod_rect_fast(lxp, lyp, r, lim, scale);
+      uint32_t k;
+      if (demod_rect_quick(r, lim, scale, k)) return k;
+      k = demod_rect_fast(lxp, lyp, r, lim, scale);
       return k < 256u ? k : demod_exhaustive(tab, r);
     } else {
       const float fx = (r.x + cR) * inv_cs, fy = (r.y + cR) * inv_cs;
@@ -707,18 +746,28 @@ GSDR_C_LINKAGE hipError_t gsdrxQpsk256ModulateAwgn(const uint8_t* inputBytes, hi
   if (scope.status() != hipSuccess) return scope.status();
   const uint32_t blocks = (uint32_t)gsdr::ceil_div<uint64_t>(numSymbols, gsdr::kAwgnBlockSyms);
   float2* out = reinterpret_cast<float2*>(output);
+  const uint64_t blk = firstSymbolIndex / 3u;
+  auto launch = [&](auto r3, auto rect) {
+    gsdr::k_c256_mod_awgn<decltype(r3)::value, decltype(rect)::value><<<dim3(blocks), dim3(gsdr::kCBlock), 0,
+                                                                         cudaStream>>>(
+        inputBytes, out, numSymbols, constellationType, sigma, seed, blk);
+  };
+  auto by_type = [&](auto r3) {
+    if (GSDR_C256_RECT_LEVELS && constellationType == 0) {
+      launch(r3, std::true_type{});
+    } else {
+      launch(r3, std::false_type{});
+    }
+  };
   switch (firstSymbolIndex % 3u) {
     case 0:
-      gsdr::k_c256_mod_awgn<0><<<dim3(blocks), dim3(gsdr::kCBlock), 0, cudaStream>>>(
-          inputBytes, out, numSymbols, constellationType, sigma, seed, firstSymbolIndex);
+      by_type(std::integral_constant<int, 0>{});
       break;
     case 1:
-      gsdr::k_c256_mod_awgn<1><<<dim3(blocks), dim3(gsdr::kCBlock), 0, cudaStream>>>(
-          inputBytes, out, numSymbols, constellationType, sigma, seed, firstSymbolIndex);
+      by_type(std::integral_constant<int, 1>{});
       break;
     default:
-      gsdr::k_c256_mod_awgn<2><<<dim3(blocks), dim3(gsdr::kCBlock), 0, cudaStream>>>(
-          inputBytes, out, numSymbols, constellationType, sigma, seed, firstSymbolIndex);
+      by_type(std::integral_constant<int, 2>{});
       break;
   }
   return gsdr::launch_status();

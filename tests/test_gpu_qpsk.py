@@ -405,3 +405,26 @@ def test_qpsk256_rect_decision_boundaries(cuda, amp):
     x = (re.ravel() + 1j * im.ravel()).astype(np.complex64)
     got = ops.qpsk256_demodulate(dev(x, cuda), 0).cpu().numpy()
     assert np.array_equal(got, o.qpsk256_demod(table, x))
+
+
+@pytest.mark.parametrize("amp", [1.0, 0.37, -2.5])
+def test_qpsk256_rect_quick_path_margin(cuda, amp):
+    """The quick per-axis decision (qpsk256.hip demod_rect_quick) accepts a symbol only when its level coordinate u
+    is more than 2^-10 of a level spacing from every midpoint: symbols on a dense grid across that margin on both
+    sides of every midpoint, at the 4|a| edge and just beyond it, decide bit for bit as the exhaustive oracle."""
+    from gsdr_amd import ops
+
+    ops.qpsk256_init(0, amp)
+    table = o.qpsk256_table(0, amp)
+    lv = np.unique(table.real.astype(np.float32)).astype(np.float64)
+    sp = (lv[-1] - lv[0]) / 15.0
+    mids = (lv[:-1] + lv[1:]) / 2
+    offs = np.concatenate([np.linspace(-3, 3, 61) * 2.0 ** -10, np.array([-0.02, 0.02, 0.3, -0.3])]) * sp
+    ax = (mids[:, None] + offs[None, :]).ravel()
+    edge = 4.0 * abs(amp)
+    ax = np.concatenate([ax, [edge, -edge, np.nextafter(np.float32(edge), np.float32(np.inf)), -edge * 1.0001]])
+    ax = np.unique(ax.astype(np.float32))
+    re, im = np.meshgrid(ax, ax)
+    x = (re.ravel() + 1j * im.ravel()).astype(np.complex64)
+    got = ops.qpsk256_demodulate(dev(x, cuda), 0).cpu().numpy()
+    assert np.array_equal(got, o.qpsk256_demod(table, x))

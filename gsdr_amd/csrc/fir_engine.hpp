@@ -106,6 +106,10 @@ struct Product<float, float> {
 
 __device__ __forceinline__ void set_zero(float& a) { a = 0.0f; }
 __device__ __forceinline__ void set_zero(float2& a) { a = make_float2(0.0f, 0.0f); }
+__device__ __forceinline__ void set_zero(Iq8& a) {
+  a.x = 0;
+  a.y = 0;
+}
 
 // Element e (compile-time after unrolling) of a 16-byte granule.
 template <class InT>
@@ -412,22 +416,44 @@ __device__ __forceinline__ typename LdsSample<InT>::type stream_sample(const InT
 }
 
 // A tile that reaches into the stream's history (only the first tile of a call: the history is shorter
-// than one window): one granule at a time through stream_sample.
+// than one window): sample by sample, each from the history or the chunk (stream_sample's rule), in batches of
+// 8 granules a thread whose loads are all issued before the first is used (one granule at a time, this tile
+// had waited on every load in turn and ran ~1 us longer than the call's other tiles).
 template <class InT, class Geo, int WG, int MODE>
 __device__ __forceinline__ void stage_tile_stream(float4* __restrict__ lds, const InT* __restrict__ in, uint64_t S0,
                                                   uint32_t NG, const FirParams& p) {
   constexpr int G = Geo::G;
-  for (uint32_t g = threadIdx.x; g < NG; g += WG) {
-    const uint64_t s = S0 + (uint64_t)g * G;
-    float4 v;
-    if constexpr (G == 2) {
-      const float2 a = stream_sample<InT>(in, p, s), b = stream_sample<InT>(in, p, s + 1);
-      v = make_float4(a.x, a.y, b.x, b.y);
-    } else {
-      v = make_float4(stream_sample<InT>(in, p, s), stream_sample<InT>(in, p, s + 1), stream_sample<InT>(in, p, s + 2),
-                      stream_sample<InT>(in, p, s + 3));
+  constexpr int B = 8;
+  const InT* __restrict__ hist = reinterpret_cast<const InT*>(p.hist);
+  for (uint32_t g0 = 0; g0 < NG; g0 += B * WG) {
+    InT v[B][G];
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      const uint32_t g = g0 + (uint32_t)b * WG + threadIdx.x;
+#pragma unroll
+      for (int e = 0; e < G; ++e) {
+        const uint64_t s = S0 + (uint64_t)g * G + (uint64_t)e;
+        const int64_t i = (int64_t)s + p.in_off;
+        if (g < NG && s < p.L) {
+          v[b][e] = i < 0 ? hist[(int64_t)p.hist_len + i] : in[s];
+        } else {
+          set_zero(v[b][e]);
+        }
+      }
     }
-    lds[Geo::padded(g)] = stage_transform<InT, MODE>(v, (uint32_t)s, p);
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      const uint32_t g = g0 + (uint32_t)b * WG + threadIdx.x;
+      if (g >= NG) break;
+      float4 w;
+      if constexpr (G == 2) {
+        const float2 a = to_lds_sample(v[b][0]), c = to_lds_sample(v[b][1]);
+        w = make_float4(a.x, a.y, c.x, c.y);
+      } else {
+        w = make_float4(v[b][0], v[b][1], v[b][2], v[b][3]);
+      }
+      lds[Geo::padded(g)] = stage_transform<InT, MODE>(w, (uint32_t)(S0 + (uint64_t)g * G), p);
+    }
   }
 }
 

@@ -24,7 +24,9 @@
 // coefficients beyond K-1 leave the recursion unchanged).
 #include <hip/hip_runtime.h>
 
+
 #include <algorithm>
+#include <atomic>
 
 #include "gsdr/iir.h"
 #include "launch.hpp"
@@ -73,6 +75,10 @@ __device__ __forceinline__ double2 shfl_up_s(double2 v, int d) {
   return make_double2(__shfl_up(v.x, d, 64), __shfl_up(v.y, d, 64));
 }
 __device__ __forceinline__ double2 add_s(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ double shfl_xor_s(double v, int d) { return __shfl_xor(v, d, 64); }
+__device__ __forceinline__ double2 shfl_xor_s(double2 v, int d) {
+  return make_double2(__shfl_xor(v.x, d, 64), __shfl_xor(v.y, d, 64));
+}
 
 struct Coeffs {
   const float* b;
@@ -81,7 +87,12 @@ struct Coeffs {
 };
 
 // coefficient i of a zero-padded array (uniform: the compiler turns these into scalar loads)
-__device__ __forceinline__ double coeff(const float* c, int K, int i) { return i < K ? (double)c[i] : 0.0; }
+// every load unconditional (clamped index, K >= 1), so the coefficient loads issue together instead of one
+// round trip each behind a branch
+__device__ __forceinline__ double coeff(const float* c, int K, int i) {
+  const float v = c[i < K ? i : K - 1];
+  return i < K ? (double)v : 0.0;
+}
 
 enum ChunkPass : int { kTails = 0, kFinal = 1 };
 
@@ -757,8 +768,58 @@ __global__ __launch_bounds__(64 * kUpperWaves) void k_iir_scan_upper(uint64_t E1
   }
 }
 
+#include "iir_resident.hpp"
+
+std::atomic<int> g_single_pass{0};
+
+// A per-call epoch for the single-pass kernel's flags (never repeats within the process; seeded from the clock
+// and the process id so stale flags of another process's allocations cannot match either).
+
+template <class S, int P>
+static hipError_t run_resident(const Coeffs& cf, S* xh, S* yh, const S* x, S* y, uint64_t n, hipStream_t st) {
+  using Sh = res::Shape<S>;
+  constexpr int NC = Sh::NC;
+  const uint64_t ntiles = ceil_div<uint64_t>(n, Sh::TS);
+  const uint64_t nsb = ceil_div<uint64_t>(ntiles, res::kResSB);
+  // one block: the tile aggregates, the superblock aggregates (both filled with kResEmpty by the setup
+  // kernel), the tables and coefficients
+  const uint64_t nagg = (ntiles + nsb) * P * NC;
+  const size_t off_tabs = nagg * sizeof(double);
+  const size_t bytes = off_tabs + (res::res_tab_doubles<P>() + res::res_coef_doubles<P>()) * sizeof(double);
+  char* ws = nullptr;
+  hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&ws), bytes, st);
+  if (e != hipSuccess) return e;
+  res::ResArgs ra{};
+  ra.loc = reinterpret_cast<double*>(ws);
+  ra.sbagg = ra.loc + ntiles * P * NC;
+  double* tabs = reinterpret_cast<double*>(ws + off_tabs);
+  ra.tabs = tabs;
+  ra.xh_out = reinterpret_cast<float*>(xh);
+  ra.yh_out = reinterpret_cast<float*>(yh);
+  ra.Pk = cf.K - 1;
+  const bool vec = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15u) == 0;
+  const uint32_t nclear = (uint32_t)std::min<uint64_t>(512, ceil_div<uint64_t>(nagg, 8 * res::kResWG));
+  res::k_res_setup<S, P><<<1 + nclear, res::kResWG, 0, st>>>(cf, tabs, reinterpret_cast<uint64_t*>(ws), nagg);
+  if (vec) {
+    res::k_iir_resident<S, P, true><<<(uint32_t)ntiles, res::kResWG, 0, st>>>(cf, x, xh, yh, n, y, ra);
+  } else {
+    res::k_iir_resident<S, P, false><<<(uint32_t)ntiles, res::kResWG, 0, st>>>(cf, x, xh, yh, n, y, ra);
+  }
+  e = launch_status();
+  const hipError_t f = hipFreeAsync(ws, st);
+  return e != hipSuccess ? e : f;
+}
+
 template <class S, int P>
 static hipError_t run(const Coeffs& cf, S* xh, S* yh, const S* x, S* y, uint64_t n, hipStream_t st) {
+  // K <= 9 and up to 2^16 tiles (2^29 real / 2^28 complex samples), when selected (gsdrxIirSetSinglePass):
+  // the single-pass kernel. Measured slower than the scan below on MI355X, so off by
+  // default.
+  if constexpr (P <= kFusedMaxP) {
+    if (g_single_pass.load(std::memory_order_relaxed) &&
+        ceil_div<uint64_t>(n, res::Shape<S>::TS) <= res::kResMaxTiles)
+      return run_resident<S, P>(cf, xh, yh, x, y, n, st);
+  }
   using A = typename Acc<S>::type;
   const uint64_t C = ceil_div<uint64_t>(n, kChunk);
   // level sizes: E[0] = C chunks, E[k+1] = ceil(E[k] / G) until one group remains
@@ -923,4 +984,8 @@ GSDR_C_LINKAGE hipError_t gsdrIirCCCustom(const float* bCoeffs, const float* aCo
   if (samplesPerThread == 0 || samplesPerThread > 32) return hipErrorInvalidValue;
   return gsdrIirCC(bCoeffs, aCoeffs, coeffCount, inputHistory, outputHistory, input, output, numElements, cudaDevice,
                    cudaStream);
+}
+
+GSDR_C_LINKAGE int gsdrxIirSetSinglePass(int enable) GSDR_NO_EXCEPT {
+  return gsdr::iir::g_single_pass.exchange(enable != 0 ? 1 : 0);
 }

@@ -19,6 +19,17 @@ pytestmark = pytest.mark.gpu
 IIR_TOL = 1e-6
 
 
+@pytest.fixture(autouse=True, params=["scan", "single_pass"])
+def iir_kernel(request, cuda):
+    """Every test runs on both IIR paths: the multi-pass scan (default) and the single-pass kernel
+    (gsdrxIirSetSinglePass; K <= 9, larger K falls back to the scan)."""
+    from gsdr_amd import abi
+
+    prev = abi.lib.gsdrxIirSetSinglePass(1 if request.param == "single_pass" else 0)
+    yield request.param
+    abi.lib.gsdrxIirSetSinglePass(prev)
+
+
 def bar(b, a, x, want, xh=None, yh=None):
     return max(IIR_TOL, 4 * err(o.iir_f32(b, a, x, xh, yh), want))
 
@@ -163,3 +174,28 @@ def test_iir_scan_paths(cuda, order, n):
     e = err(y, want)
     print(f"order={order} n={n} err={e:.2e}")
     assert e <= IIR_TOL
+
+
+@pytest.mark.parametrize("order", [1, 2])
+@pytest.mark.parametrize("n", [3 * 8192 + 1, 3 * (1 << 21) + 5])
+@pytest.mark.parametrize("cplx", [False, True])
+def test_iir_slow_decay_carries(cuda, order, n, cplx):
+    """Poles at radius 1 - 1e-6: the state entering a tile carries weight ~e^-2 across a superblock of 2^21
+    samples, so a carry dropped or misordered anywhere in the single-pass scan (chunks within a wave,
+    waves within a tile, tiles within a superblock, superblocks) shows at O(1) rather than under the
+    tolerance, as it would for a fast-decaying filter. DC input plus noise keeps the output O(1)."""
+    from gsdr_amd import ops
+
+    r = 1.0 - 1e-6
+    a = np.poly([r] if order == 1 else [r * np.exp(3e-3j), r * np.exp(-3e-3j)]).real.astype(np.float32)
+    b = np.zeros(order + 1, np.float32)
+    b[0] = np.float32(np.sum(a.astype(np.float64)))  # unit DC gain
+    rng = np.random.default_rng(n + order)
+    x = rng.uniform(0, 1, n).astype(np.float32)
+    if cplx:
+        x = (x + 1j * rng.uniform(-1, 0, n)).astype(np.complex64)
+    y = ops.iir(dev(b, cuda), dev(a, cuda), dev(x, cuda)).cpu().numpy()
+    want, _, _ = o.iir(b, a, x)
+    e = float(np.max(np.abs(y - want))) / float(np.max(np.abs(want)))
+    print(f"order={order} n={n} cplx={cplx} err={e:.2e} peak={float(np.max(np.abs(want))):.3g}")
+    assert e <= 1e-5

@@ -58,6 +58,7 @@ def main():
     from scipy import signal as sps
 
     bb, aa = (torch.tensor(v, dtype=torch.float32, device=dev) for v in sps.butter(4, 0.1))
+    bb8, aa8 = (torch.tensor(v, dtype=torch.float32, device=dev) for v in sps.butter(8, 0.2))
     xi = torch.rand(n5, device=dev, generator=g)
     yi = torch.empty_like(xi)
     xic = torch.rand(2 * n5, device=dev, generator=g).view(torch.complex64)
@@ -81,6 +82,10 @@ def main():
                                                   yi.data_ptr(), n5, 0, st),
         "gsdrIirCC": lambda lib, k: lib.gsdrIirCC(bb.data_ptr(), aa.data_ptr(), 5, None, None, xic.data_ptr(),
                                                   yic.data_ptr(), n5, 0, st),
+        "gsdrIirFF9": lambda lib, k: lib.gsdrIirFF(bb8.data_ptr(), aa8.data_ptr(), 9, None, None, xi.data_ptr(),
+                                                   yi.data_ptr(), n5, 0, st),
+        "gsdrIirCC9": lambda lib, k: lib.gsdrIirCC(bb8.data_ptr(), aa8.data_ptr(), 9, None, None, xic.data_ptr(),
+                                                   yic.data_ptr(), n5, 0, st),
     }
     only = os.environ.get("CASES")
     res = {}

@@ -117,6 +117,9 @@ __device__ __forceinline__ void awgn_load_table(AwgnLds& t, uint32_t nthreads) {
   }
 }
 __device__ __forceinline__ float awgn_fma(const AwgnLds& t, uint32_t i, float f) {
+#if defined(GSDR_TUNING_PROBES) && defined(GSDR_AWGN_PROBE_NOGATHER)
+  i = 256u + (threadIdx.x & 63u) + (i & 0x100u);  // timing probe only: conflict-free, no tail entries, wrong noise
+#endif
 #ifdef GSDR_AWGN_PAIRS
   const float2 e = t.rs[i];
   return fmaf(e.y, f, e.x);

@@ -361,7 +361,11 @@ __global__ __launch_bounds__(kCBlock) void k_c256_mod_awgn(const uint8_t* __rest
 #pragma unroll
       for (int j = 0; j < kAwgnSym; ++j) {
         const float2 g = awgn_slot_main(ntab, w[(R3 + j) / 3], (R3 + j) % 3);
+#if defined(GSDR_TUNING_PROBES) && defined(GSDR_C256_PROBE_NOSYMGATHER)
+        const float2 p = tab[(lane + (sym[j] & 0x80u)) & 255u];  // timing probe only: conflict-free, wrong symbols
+#else
         const float2 p = RECT ? make_float2(lev[sym[j] >> 4], lev[16 + (sym[j] & 15)]) : tab[sym[j]];
+#endif
         y[j] = make_float2(p.x + sigma * g.x, p.y + sigma * g.y);
       }
     }

@@ -500,11 +500,21 @@ hipError_t launch_poly_default(const FirJob& j, hipStream_t s) {
 // 23.5 / 8.9 / 5.7, WG 256 R 1 29.2 / 9.9 / 5.1 -- so calls of fewer than three rounds of 1,024-output
 // tiles take R 2. The per-output MAC order depends only on (D, JC): every shape gives the same outputs bit
 // for bit.
+#ifndef GSDR_SHORT_R1
+#define GSDR_SHORT_R1 1
+#endif
 template <class TapT, class InT, int MODE>
 hipError_t launch_poly_d4(const FirJob& j, hipStream_t s) {
   int cus = 0;
   if (current_device_cus(&cus) == hipSuccess && cus > 0) {
     const uint64_t slots = (uint64_t)cus * 4;  // 38 KB tiles: 4 workgroups a CU
+#if GSDR_SHORT_R1
+    // calls of at most one 256-output tile for every second slot (2^19 input samples at D = 4 on 256 CUs):
+    // 256-output tiles (same JC: the same outputs bit for bit). Measured per FM call (tools/short_call_floor.py):
+    // 2^16 / 2^18 samples 5.41 / 5.51 -> 4.74 / 4.89 us direct, 7.98 / 7.71 -> 5.95 / 5.96 us as a stream call;
+    // at 2^20 samples (one such tile a slot) 6.93 -> 8.39 us, so larger calls keep the 512-output tiles
+    if (2 * ceil_div<uint64_t>(j.N, 256) <= slots) return launch_poly<TapT, InT, 4, 1, 16, 256, MODE, 0, true>(j, s);
+#endif
     if (ceil_div<uint64_t>(j.N, 1024) < 3 * slots) return launch_poly<TapT, InT, 4, 2, 16, 256, MODE, 0, true>(j, s);
   }
   return launch_poly_default<TapT, InT, 4, 4, 16, 256, MODE>(j, s);

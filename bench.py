@@ -756,7 +756,15 @@ def main():
     # BENCH_REHEARSE=1 (rehearsal only, never a reported number): gloo instead of RCCL and rank r on
     # cuda:(r mod device_count), so the N > 1 code path can run on a one-GPU box with ranks sharing it.
     rehearse = os.environ.get("BENCH_REHEARSE") == "1"
-    dev_index = local_rank % torch.cuda.device_count() if rehearse else local_rank
+    ndev = torch.cuda.device_count()
+    if rehearse:
+        dev_index = local_rank % ndev
+    elif local_rank < ndev:
+        dev_index = local_rank
+    elif ndev == 1:
+        dev_index = 0  # one visible device per rank (a per-rank HIP_VISIBLE_DEVICES); validate_ranks checks they differ
+    else:
+        raise SystemExit(f"local rank {local_rank} but only {ndev} visible devices")
     torch.cuda.set_device(dev_index)
     device = torch.device("cuda", dev_index)
     if world > 1:

@@ -33,10 +33,19 @@ if stats:
     d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3 for r in csv.DictReader(open(trace))
          if r["Kernel_Name"].startswith(fir_name)]
     if d:
-        timed_mean = sum(d[-a.steps:]) / len(d[-a.steps:])
+        # the timed steps are dispatches [W + settle, W + settle + K) of the headline kernel: the profiled run's
+        # own line says how many warm-up and clock-settle launches preceded them
+        lo, what = len(d) - a.steps, f"the last {a.steps}"
+        pl = os.path.join(ROOT, "gpurun_out", "bench_profiled.json")
+        if os.path.exists(pl):
+            line = json.loads(open(pl).read().strip().splitlines()[-1])
+            lo = int(line.get("warmup", 0)) + int(line.get("clock_settle_launches", 0))
+            what = f"dispatches {lo}..{lo + a.steps - 1} (after {line.get('warmup')} warm-up and {line.get('clock_settle_launches')} clock-settle launches)"
+        w = d[lo:lo + a.steps]
+        timed_mean = sum(w) / len(w)
         with open(os.path.join(prof, f"{a.tag}_bench_fir_dispatches.txt"), "w") as f:
             f.write(f"# {fir_name}: per-dispatch duration (us) from rocprofv3 --kernel-trace of `python bench.py`\n")
-            f.write(f"# dispatches {len(d)}; mean of the last {a.steps} (the timed steps) = {timed_mean:.2f} us\n")
+            f.write(f"# dispatches {len(d)}; the timed steps = {what}: mean {timed_mean:.2f} us\n")
             f.write("\n".join(f"{x:.2f}" for x in d) + "\n")
 prof_line = os.path.join(ROOT, "gpurun_out", "bench_profiled.json")
 if os.path.exists(prof_line):  # the profiled run's own bench line (gpu_round.sh), to set beside the trace

@@ -457,16 +457,36 @@ __device__ __forceinline__ void stage_tile_stream(float4* __restrict__ lds, cons
   }
 }
 
-// The next history of a streaming call, copied by workgroup 0 (any time during the launch: it writes
-// the stream's spare buffer, which no tile reads).
+// The next history of a streaming call, copied by workgroup 0 (it writes the stream's spare buffer, which no
+// tile reads). Split so that it costs the workgroup no round trip of its own: each thread loads its sample
+// before the tile's loads are issued (stream_history_load) and stores it after the staging, whose waits
+// have covered that load (stream_history_store). Histories longer than the workgroup (T + D > WG samples)
+// copy the rest there with a plain loop.
 template <class InT>
-__device__ __forceinline__ void stream_copy_history(const FirParams& p) {
+struct HistSample {
+  InT v;
+  bool on;
+};
+template <class InT>
+__device__ __forceinline__ HistSample<InT> stream_history_load(const FirParams& p) {
+  HistSample<InT> h{};
+  h.on = p.hist_out != nullptr && blockIdx.x == 0 && threadIdx.x < p.hist_n;
+  if (h.on) {
+    const int64_t i = p.hist_from + (int64_t)threadIdx.x;  // chunk offset
+    h.v = i < 0 ? reinterpret_cast<const InT*>(p.hist)[(int64_t)p.hist_len + i]
+                : reinterpret_cast<const InT*>(p.in)[i - p.in_off];
+  }
+  return h;
+}
+template <class InT>
+__device__ __forceinline__ void stream_history_store(const FirParams& p, const HistSample<InT>& h) {
   if (p.hist_out == nullptr || blockIdx.x != 0) return;
-  const InT* __restrict__ in = reinterpret_cast<const InT*>(p.in);  // chunk + in_off
   InT* __restrict__ dst = reinterpret_cast<InT*>(p.hist_out);
-  for (uint64_t j = threadIdx.x; j < p.hist_n; j += blockDim.x) {
-    const int64_t i = p.hist_from + (int64_t)j;  // chunk offset
-    dst[j] = i < 0 ? reinterpret_cast<const InT*>(p.hist)[(int64_t)p.hist_len + i] : in[i - p.in_off];
+  if (h.on) dst[threadIdx.x] = h.v;
+  for (uint64_t j = threadIdx.x + blockDim.x; j < p.hist_n; j += blockDim.x) {
+    const int64_t i = p.hist_from + (int64_t)j;
+    dst[j] = i < 0 ? reinterpret_cast<const InT*>(p.hist)[(int64_t)p.hist_len + i]
+                   : reinterpret_cast<const InT*>(p.in)[i - p.in_off];
   }
 }
 
@@ -1093,7 +1113,7 @@ __device__ __forceinline__ void fir_poly_tile(const FirParams& p, uint32_t tile)
 
   extern __shared__ __attribute__((aligned(16))) float4 lds[];
   const InT* __restrict__ in = reinterpret_cast<const InT*>(p.in);
-  stream_copy_history<InT>(p);
+  const HistSample<InT> hist = stream_history_load<InT>(p);
 
   const uint64_t out0 = (uint64_t)tile * p.tile_stride;
   const uint64_t S0 = out0 * D;
@@ -1105,6 +1125,7 @@ __device__ __forceinline__ void fir_poly_tile(const FirParams& p, uint32_t tile)
     stage_tile<InT, Geo, WG, VEC, SMODE, NT, DMA, SH, (ABL & 32) != 0, (ABL & 128) != 0>(lds, in, S0, NG, p);
   }
   __syncthreads();
+  stream_history_store<InT>(p, hist);
 
   OutT acc[R];
 #pragma unroll
@@ -1267,7 +1288,7 @@ __global__ __launch_bounds__(WG) void k_fir_contig(FirParams p) {
 
   extern __shared__ __attribute__((aligned(16))) float4 lds[];
   const InT* __restrict__ in = reinterpret_cast<const InT*>(p.in);
-  stream_copy_history<InT>(p);
+  const HistSample<InT> hist = stream_history_load<InT>(p);
 
   const uint64_t out0 = (uint64_t)blockIdx.x * p.tile_stride;
   const uint64_t S0 = out0 * D;
@@ -1276,6 +1297,7 @@ __global__ __launch_bounds__(WG) void k_fir_contig(FirParams p) {
 
   stage_tile<InT, Geo, WG, VEC, MODE, false, false, SH>(lds, in, S0, NG, p);
   __syncthreads();
+  stream_history_store<InT>(p, hist);
 
   OutT acc[R];
 #pragma unroll

@@ -18,6 +18,7 @@ REPS = int(os.environ.get("REPS", "30"))
 f, u32, i32, p, sz, u64 = ctypes.c_float, ctypes.c_uint32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64
 SIGS = {
     "gsdrFirFC": [sz, p, sz, p, p, sz, i32, p],
+    "gsdrFirFF": [sz, p, sz, p, p, sz, i32, p],
     "gsdrFmDemod": [f, f, f, f, u32, sz, p, sz, p, p, sz, i32, p],
     "gsdrxFmDemodInt8": [f, f, f, f, u32, sz, p, sz, p, p, sz, i32, p],
     "gsdrxAmDemodInt8": [f, f, f, u32, sz, p, sz, p, p, sz, i32, p],
@@ -52,6 +53,9 @@ def main():
     yc = torch.empty(NO, dtype=torch.complex64, device=dev)
     yf = torch.empty(NO, dtype=torch.float32, device=dev)
     n5 = 1 << 24
+    t1 = torch.rand(63, device=dev, generator=g)  # config 1: 2^20 real outputs, 63 taps, D = 1
+    x1 = torch.rand((1 << 20) + 62, device=dev, generator=g)
+    y1 = torch.empty(1 << 20, device=dev)
     syms = torch.randint(0, 256, (n5,), dtype=torch.uint8, device=dev, generator=g)
     rx = torch.empty(n5, dtype=torch.complex64, device=dev)
     dec = torch.empty(n5, dtype=torch.uint8, device=dev)
@@ -66,6 +70,7 @@ def main():
     for lib in L:
         assert lib.gsdrQpsk256InitConstellation(0, 1.0, 0, st) == 0
     cases = {
+        "gsdrFirFF1": lambda lib, k: lib.gsdrFirFF(1, t1.data_ptr(), 63, x1.data_ptr(), y1.data_ptr(), 1 << 20, 0, st),
         "gsdrFirFC": lambda lib, k: lib.gsdrFirFC(D, taps.data_ptr(), T, xs[k % 2].data_ptr(), yc.data_ptr(), NO, 0, st),
         "gsdrFmDemod": lambda lib, k: lib.gsdrFmDemod(1e6, 0.0, 1e5, 2e4, D, 0, taps.data_ptr(), T, xs[k % 2].data_ptr(),
                                                       yf.data_ptr(), NO - 1, 0, st),

@@ -83,6 +83,10 @@ def main():
         "gsdrxQpsk256ModulateAwgn": lambda lib, k: lib.gsdrxQpsk256ModulateAwgn(syms.data_ptr(), rx.data_ptr(), n5, 0,
                                                                                 0.02, 0x5EED0005, 0, 0, st),
         "gsdrQpsk256Demodulate": lambda lib, k: lib.gsdrQpsk256Demodulate(rx.data_ptr(), dec.data_ptr(), n5, 0, 0, st),
+        # config 5's round trip: modulate + AWGN, then demodulate what it wrote
+        "config5_round_trip": lambda lib, k: (lib.gsdrxQpsk256ModulateAwgn(syms.data_ptr(), rx.data_ptr(), n5, 0, 0.02,
+                                                                           0x5EED0005, 0, 0, st),
+                                              lib.gsdrQpsk256Demodulate(rx.data_ptr(), dec.data_ptr(), n5, 0, 0, st))[1],
         "gsdrIirFF": lambda lib, k: lib.gsdrIirFF(bb.data_ptr(), aa.data_ptr(), 5, None, None, xi.data_ptr(),
                                                   yi.data_ptr(), n5, 0, st),
         "gsdrIirCC": lambda lib, k: lib.gsdrIirCC(bb.data_ptr(), aa.data_ptr(), 5, None, None, xic.data_ptr(),

@@ -606,6 +606,21 @@ def secondary_configs(torch, ops, device, taps):
     ta = s4.elapsed_time(e4) / reps * 1e-3
     ops.qpsk256_demodulate(tx, 0, out=rx_bytes)
     torch.cuda.synchronize()
+    # the round trip as a pipeline (each demodulation reads the buffer its modulation just wrote), beside the
+    # sum of the two kernels timed apart
+    # (the C-ABI calls with pre-marshalled arguments: two Python wrapper calls an iteration would be host-bound)
+    st5 = torch.cuda.current_stream(device).cuda_stream
+    fmod, fdem = abi.lib.gsdrxQpsk256ModulateAwgn, abi.lib.gsdrQpsk256Demodulate
+    amod = (syms.data_ptr(), tx.data_ptr(), n, 0, sigma, seed, 0, device.index, st5)
+    adem = (tx.data_ptr(), rx_bytes.data_ptr(), n, 0, device.index, st5)
+    s5, e5 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s5.record()
+    for _ in range(reps):
+        fmod(*amod)
+        fdem(*adem)
+    e5.record()
+    torch.cuda.synchronize()
+    out["qpsk256"]["round_trip_pipelined_us"] = round(s5.elapsed_time(e5) / reps * 1e3, 2)
     out["qpsk256"]["modulate_awgn_us"] = round(ta * 1e6, 2)
     out["qpsk256"]["round_trip_us"] = round((ta + td) * 1e6, 2)
     out["qpsk256"]["round_trip_msymbols_per_s"] = round(n / (ta + td) / 1e6, 1)

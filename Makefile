@@ -22,15 +22,19 @@ $(BUILD)/%.o: gsdr_amd/csrc/%.hip $(HDRS)
 gsdr_amd/libgsdr.so: $(OBJS)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -Wl,-rpath,/opt/rocm/lib $(OBJS) -o $@
 
-# Tuning-probe build (ablation variants >= 100 of gsdrxFirFCVariant): the product objects with fir.hip
-# recompiled under GSDR_TUNING_PROBES. Loaded by tools/ through GSDR_LIB; never by the tests or bench.
+# Tuning-probe build: the product objects with fir.hip (ablation variants >= 100 of gsdrxFirFCVariant) and iir.hip
+# (the single-pass IIR, gsdrxIirFFSinglePass / CC) recompiled under GSDR_TUNING_PROBES. Loaded by tools/, by
+# bench.py's staging-ceiling leg and by tests/test_gpu_iir_single_pass.py; never by the product path.
 probes: $(BUILD)/probes/libgsdr_probes.so
 
-$(BUILD)/probes/fir.o: gsdr_amd/csrc/fir.hip $(HDRS)
+PROBE_SRCS := fir iir
+PROBE_OBJS := $(patsubst %,$(BUILD)/probes/%.o,$(PROBE_SRCS))
+
+$(BUILD)/probes/%.o: gsdr_amd/csrc/%.hip $(HDRS)
 	@mkdir -p $(BUILD)/probes
 	$(HIPCC) $(HIPFLAGS) -DGSDR_TUNING_PROBES -c $< -o $@
 
-$(BUILD)/probes/libgsdr_probes.so: $(filter-out $(BUILD)/fir.o,$(OBJS)) $(BUILD)/probes/fir.o
+$(BUILD)/probes/libgsdr_probes.so: $(filter-out $(patsubst %,$(BUILD)/%.o,$(PROBE_SRCS)),$(OBJS)) $(PROBE_OBJS)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -Wl,-rpath,/opt/rocm/lib $^ -o $@
 
 oracle/build/liboracle.so: oracle/gsdr_oracle.c oracle/gsdr_oracle.h gsdr_amd/csrc/awgn_table.inc gsdr_amd/csrc/awgn_tail_table.inc
@@ -38,9 +42,13 @@ oracle/build/liboracle.so: oracle/gsdr_oracle.c oracle/gsdr_oracle.h gsdr_amd/cs
 	$(CC) $(OFLAGS) -shared oracle/gsdr_oracle.c -o $@ -lm -lpthread
 
 # C++ host example linking the C ABI
-examples: $(BUILD)/fm_receiver
+examples: $(BUILD)/fm_receiver $(BUILD)/short_call_timer
 
 $(BUILD)/fm_receiver: examples/fm_receiver.cpp gsdr_amd/libgsdr.so $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) -O2 -std=c++17 -Iinclude $< -Lgsdr_amd -lgsdr -Wl,-rpath,'$$ORIGIN/../gsdr_amd' -o $@
+
+$(BUILD)/short_call_timer: examples/short_call_timer.cpp gsdr_amd/libgsdr.so $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) -O2 -std=c++17 -Iinclude $< -Lgsdr_amd -lgsdr -Wl,-rpath,'$$ORIGIN/../gsdr_amd' -o $@
 

@@ -97,7 +97,6 @@ SIGNATURES = {
     "gsdrxStreamDestroy": (_err, [_p]),
     "gsdrxStreamPlan": (None, [_u32, _sz, ctypes.c_uint64, ctypes.c_uint64, _sz, ctypes.POINTER(ctypes.c_uint64)]),
     "gsdrxAmDemodInt8": (_err, [_f, _f, _f, _u32, _sz, _p, _sz, _p, _p, _sz, _i32, _p]),
-    "gsdrxIirSetSinglePass": (ctypes.c_int, [ctypes.c_int]),
 }
 
 

@@ -68,15 +68,13 @@ hipError_t launch_fc_probe(const FirJob& j, hipStream_t s) {
     case 117:  // staging only by LDS-DMA, non-temporal
       return launch_poly<float, float2, 4, 4, 16, 256, kModeFir, 1, true, false, 0, true>(j, s);
     // FM chain (config 3 shape) split: 120 full FM kernel, 121 no NCO mix, 122 no discriminator (plain
-    // float store), 123 neither, 124 staging + NCO + discriminator without the FIR, 125 staging only,
-    // 126 NCO mix without its per-granule transcendental pair
+    // float store), 123 neither, 124 staging + NCO + discriminator without the FIR, 125 staging only
     case 120:
     case 121:
     case 122:
     case 123:
     case 124:
-    case 125:
-    case 126: {
+    case 125: {
       FirJob c = j;
       c.mode = kModeFm;
       c.N = j.N - 1;  // an FM output needs one more FIR output than the input holds for N FIR outputs
@@ -88,7 +86,6 @@ hipError_t launch_fc_probe(const FirJob& j, hipStream_t s) {
         case 122: return launch_poly<float, float2, 4, 4, 16, 256, kModeFm, 16, true>(c, s);
         case 123: return launch_poly<float, float2, 4, 4, 16, 256, kModeFm, 24, true>(c, s);
         case 124: return launch_poly<float, float2, 4, 4, 16, 256, kModeFm, 1, true>(c, s);
-        case 126: return launch_poly<float, float2, 4, 4, 16, 256, kModeFm, 32, true>(c, s);
         default: return launch_poly<float, float2, 4, 4, 16, 256, kModeFm, 25, true>(c, s);
       }
     }
@@ -123,36 +120,6 @@ hipError_t launch_fc_probe(const FirJob& j, hipStream_t s) {
       return launch_poly<float, float2, 4, 4, 16, 256, kModeFir, 64, true>(j, s);
     case 141:
       return launch_poly<float, float2, 4, 4, 16, 256, kModeFir, 66, true>(j, s);
-    // FM chain: 127 tile-relative NCO phasors by recurrence (one cmul a granule instead of the
-    // transcendental pair)
-    case 127: {
-      FirJob c = j;
-      c.mode = kModeFm;
-      c.N = j.N - 1;
-      c.nco_inc = 429496730u;
-      c.fm_gain = 7.957747f;
-      return launch_poly<float, float2, 4, 4, 16, 256, kModeFm, 128, true>(c, s);
-    }
-    // 128: persistent workgroups with tile-relative NCO phasors held in registers (k_fir_poly_rel)
-    case 128: {
-      FirJob c = j;
-      c.mode = kModeFm;
-      c.N = j.N - 1;
-      c.nco_inc = 429496730u;
-      c.fm_gain = 7.957747f;
-      using Geo = TileGeo<float2, 4, 4, 256>;
-      FirParams p = make_params(c);
-      p.nch = 2;
-      p.tile_stride = Geo::KT - 1;
-      const uint32_t tiles = (uint32_t)ceil_div<uint64_t>(c.N, p.tile_stride);
-      int cus = 0;
-      const hipError_t e = current_device_cus(&cus);
-      if (e != hipSuccess) return e;
-      const uint32_t grid = std::min<uint32_t>(tiles, (uint32_t)cus * 4u);
-      const size_t lds = poly_lds_bytes<float2, 4, 4, 256>(128, kModeFm);
-      k_fir_poly_rel<float, float2, 4, 4, 16, 256, kModeFm><<<dim3(grid), dim3(256), lds, s>>>(p, tiles);
-      return launch_status();
-    }
     case 110:
     case 111:
       return launch_stream_probe(j, s, j.variant == 111);

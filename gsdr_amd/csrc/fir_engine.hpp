@@ -195,6 +195,10 @@ struct FirParams {
   uint32_t nco_n0;       // low 32 bits of firstSampleIndex
   float fm_gain;         // FM discriminator gain
   uint32_t out_phase;    // absolute index of output 0 mod 16 (the int8 matrix-core kernels' block grid)
+  // Anchored chains (the polyphase kernels in FM / AM mode, anchored_nco below): tile t covers outputs
+  // [t KT - tile_shift, (t + 1) KT - tile_shift) of the call, and tile 0 is sub-tile cell_sub0 of its NCO cell.
+  uint32_t tile_shift;
+  uint32_t cell_sub0;
   // The streaming object's one-launch path (stream.hip): output 0's window starts at sample in_off of the
   // caller's chunk; chunk samples at negative offsets i >= -hist_len come from hist[hist_len + i] (the
   // stream's history), and samples [hist_from, hist_from + hist_n) (same offsets) are copied to hist_out
@@ -275,6 +279,9 @@ __device__ __forceinline__ float4 load16_nt(const float4* p) {
 template <class InT, bool VEC>
 __device__ __forceinline__ float4 load_granule(const InT* __restrict__ in, uint64_t s, uint64_t L) {
   constexpr int G = SampleT<InT>::kPerGranule;
+  // (an anchored chain's first tile starts before the call's first sample: its local indices below 0 arrive
+  // wrapped, and those granules -- whole granules, since tiles start at even samples -- read as zero)
+  if ((int64_t)s < 0) return make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   if constexpr (std::is_same<InT, Iq8>::value) {
     if (VEC && s + 2 <= L) return iq8x2_granule(*reinterpret_cast<const uint32_t*>(in + s));
     float2 a = make_float2(0.0f, 0.0f), b = a;
@@ -310,16 +317,13 @@ __device__ __forceinline__ float4 load_granule(const InT* __restrict__ in, uint6
 // its first sample; `odd` = n & 1 (wave-uniform in the tiled kernels: they stage granules at even
 // offsets from the tile start). The phasor is a pure function of the absolute index: even n from
 // nco_direct, odd n = phasor(n - 1) * w, w = nco_direct(inc).
-template <class InT, int MODE, bool NODIRECT = false>
+template <class InT, int MODE>
 __device__ __forceinline__ float4 stage_transform_ph(float4 v, uint32_t ph, bool odd, uint32_t inc) {
   if constexpr (MODE != kModeFir) {
     static_assert(SampleT<InT>::kPerGranule == 2, "NCO modes take complex input");
     const float2 w = nco_direct(inc);
     float2 ea, eb;
-    if constexpr (NODIRECT) {  // tuning probe only: the per-granule transcendental pair left out
-      ea = make_float2(w.y, w.x);
-      eb = cmul(ea, w);
-    } else if (odd) {
+    if (odd) {
       ea = cmul(nco_direct(ph - inc), w);
       eb = nco_direct(ph + inc);
     } else {
@@ -496,8 +500,7 @@ __device__ __forceinline__ void stream_history_store(const FirParams& p, const H
 // split over two LDS granules (second half of slot g - 1, first half of slot g); the halo re-writes the
 // body's last slot whole. The NCO phasor is a function of the absolute index, so the odd-start pairs
 // mix exactly as the even-start ones would.
-template <class InT, class Geo, int WG, bool VEC, int MODE, bool NT = false, bool DMA = false, int SH = 0,
-          bool NODIRECT = false, bool REL = false>
+template <class InT, class Geo, int WG, bool VEC, int MODE, bool NT = false, bool DMA = false, int SH = 0>
 __device__ __forceinline__ void stage_tile(float4* __restrict__ lds, const InT* __restrict__ in, uint64_t S0,
                                            uint32_t NG, const FirParams& p) {
   constexpr int G = Geo::G;
@@ -514,7 +517,7 @@ __device__ __forceinline__ void stage_tile(float4* __restrict__ lds, const InT* 
   const uint32_t tid = threadIdx.x;
   const PhaseWalk pw = phase_walk<G, WG>(p.nco_n0, S0, p.nco_inc);
   // wave-uniform: is the whole staged span readable? (every tile but the last)
-  const bool whole = VEC && (S0 + (uint64_t)NG * G <= p.L);
+  const bool whole = VEC && (int64_t)S0 >= 0 && (S0 + (uint64_t)NG * G <= p.L);
   if constexpr (SH != 0 && std::is_same<InT, float>::value) {
     // real samples SH (1..3) floats off 16-byte alignment (4-byte aligned): aligned 16-byte loads from
     // SH samples early; loaded quad g holds the last SH samples of granule g - 1 and the first 4 - SH of
@@ -618,42 +621,6 @@ __device__ __forceinline__ void stage_tile(float4* __restrict__ lds, const InT* 
   // The body loop, instantiated once per NCO start parity (`odd` is uniform over the tile): with the
   // parity a runtime value the compiler kept a branch around every granule's phasor.
   const uint32_t pbase = Geo::padded(tid);
-  if constexpr (REL && MODE != kModeFir) {
-    // tuning probe: tile-relative phasors by recurrence (granule k * WG + tid starts at tile-relative
-    // sample G (k WG + tid): its phasor is the previous granule's times F = phasor(G WG))
-    static_assert(G == 2, "complex samples");
-    const float2 w = nco_direct(p.nco_inc), F = nco_direct((uint32_t)(WG * G) * p.nco_inc);
-    float2 ea = nco_direct((uint32_t)(G * tid) * p.nco_inc);
-#pragma unroll
-    for (int b0 = 0; b0 < BPT; b0 += SB) {
-      float4 v[SB];
-      const float4* __restrict__ src = reinterpret_cast<const float4*>(in + S0);
-      if (whole) {
-#pragma unroll
-        for (int k = 0; k < SB; ++k) v[k] = load16_nt(src + (b0 + k) * WG + tid);
-      } else {
-#pragma unroll
-        for (int k = 0; k < SB; ++k) v[k] = load_granule<InT, VEC>(in, S0 + (uint64_t)((b0 + k) * WG + tid) * G, p.L);
-      }
-#pragma unroll
-      for (int k = 0; k < SB; ++k) {
-        if (b0 + k > 0) ea = cmul(ea, F);
-        const float2 eb = cmul(ea, w);
-        const float2 a = cmul(make_float2(v[k].x, v[k].y), ea);
-        const float2 b = cmul(make_float2(v[k].z, v[k].w), eb);
-        lds[pbase + (uint32_t)(b0 + k) * Geo::padded(WG)] = make_float4(a.x, a.y, b.x, b.y);
-      }
-    }
-    for (uint32_t g = BPT * WG + tid; g < NG; g += WG) {
-      ea = cmul(ea, F);
-      const float4 v = load_granule<InT, VEC>(in, S0 + (uint64_t)g * G, p.L);
-      const float2 eb = cmul(ea, w);
-      const float2 a = cmul(make_float2(v.x, v.y), ea);
-      const float2 b = cmul(make_float2(v.z, v.w), eb);
-      lds[Geo::padded(g)] = make_float4(a.x, a.y, b.x, b.y);
-    }
-    return;
-  }
   auto body = [&](auto odd_c) {
     constexpr bool ODD = decltype(odd_c)::value;
 #pragma unroll
@@ -692,7 +659,7 @@ __device__ __forceinline__ void stage_tile(float4* __restrict__ lds, const InT* 
       // padded(k * WG + tid) = padded(tid) + k * padded(WG) when whole segments fit a workgroup's row of
       // granules: a per-thread base plus an immediate offset per granule
       const uint32_t slot = (WG % Geo::SG == 0) ? pbase + (uint32_t)(b0 + k) * Geo::padded(WG) : Geo::padded(g);
-      lds[slot] = stage_transform_ph<InT, MODE, NODIRECT>(v[k], pw.ph0 + (uint32_t)(b0 + k) * pw.step, ODD, pw.inc);
+      lds[slot] = stage_transform_ph<InT, MODE>(v[k], pw.ph0 + (uint32_t)(b0 + k) * pw.step, ODD, pw.inc);
     }
   }
   };
@@ -706,6 +673,179 @@ __device__ __forceinline__ void stage_tile(float4* __restrict__ lds, const InT* 
   for (uint32_t g = BPT * WG + tid; g < NG; g += WG) {
     const uint64_t s = S0 + (uint64_t)g * G;
     lds[Geo::padded(g)] = stage_transform<InT, MODE>(load_granule<InT, VEC>(in, s, p.L), (uint32_t)s, p);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Anchored NCO (the polyphase kernels in FM / AM mode). The FM discriminator and the AM envelope are
+// invariant to a rotation common to the FIR outputs they combine, so a tile need not mix with the absolute
+// phasor e^(j 2 pi P(n) / 2^32): it may mix relative to an anchor sample, as long as every output and its
+// discriminator partner share the anchor. The anchors form an absolute grid: output q (absolute index
+// q = firstSampleIndex / D + m) belongs to cell q / CELL (CELL = the decimation's largest tile, 1,024 outputs
+// at D = 4), and all of a cell's FIR outputs -- in FM mode also the first output of the next cell, which the
+// cell's last discriminator pairs with -- come from samples mixed relative to the cell's first sample.
+// Within a cell, granule (row k, lane l) (samples 2 (k WG + l) and 2 (k WG + l) + 1 after the anchor) takes the
+// phasors e_k(l) and e_k(l) w, with e_0(l) = E(2 l), e_k(l) = e_(k-1)(l) F, F = E(2 WG), w = E(1) (E: the exact
+// integer phase through v_cos / v_sin, nco_direct): one complex multiply a granule instead of the absolute
+// scheme's transcendental pair, and every phasor a fixed sequence of operations on (l, k) alone. The
+// short-call tiles are sub-tiles of a cell that start their chains at row r0 by r0 multiplies, and every
+// staging path (aligned, shifted, streaming) forms the same values, so every tile shape and any split of a
+// stream into calls give bit-identical outputs.
+// ------------------------------------------------------------------------------------------------
+template <int WG>
+__device__ __forceinline__ float2 rel_chain_start(uint32_t lane, uint32_t rows, uint32_t inc) {
+  const float2 F = nco_direct((uint32_t)(2 * WG) * inc);
+  float2 e = nco_direct((2u * lane) * inc);
+  for (uint32_t i = 0; i < rows; ++i) e = cmul(e, F);
+  return e;
+}
+
+// a granule (two complex samples) mixed with (e, e w)
+__device__ __forceinline__ float4 rel_mix(float4 v, float2 e, float2 w) {
+  const float2 eb = cmul(e, w);
+  const float2 a = cmul(make_float2(v.x, v.y), e);
+  const float2 b = cmul(make_float2(v.z, v.w), eb);
+  return make_float4(a.x, a.y, b.x, b.y);
+}
+
+// stage_tile for an anchored chain: row0 = the cell row of the tile's first granule row. Granule g of the tile is
+// row g / WG, lane g % WG of the staging (the same map as stage_tile), so a lane walks its chain one multiply a row.
+template <class InT, class Geo, int WG, bool VEC, bool NT, int SH>
+__device__ __forceinline__ void stage_tile_rel(float4* __restrict__ lds, const InT* __restrict__ in, uint64_t S0,
+                                               uint32_t NG, const FirParams& p, uint32_t row0) {
+  constexpr int G = Geo::G;
+  static_assert(G == 2, "NCO modes take complex samples");
+  constexpr int BPT = Geo::SG * (Geo::KT / Geo::ROUT) / WG;  // body rows
+  static_assert(BPT * WG == Geo::SG * (Geo::KT / Geo::ROUT), "tile body must split evenly over the threads");
+  constexpr int SB = staging_batch(BPT);
+  const uint32_t tid = threadIdx.x;
+  const float2 w = nco_direct(p.nco_inc), F = nco_direct((uint32_t)(2 * WG) * p.nco_inc);
+  float2 e = rel_chain_start<WG>(tid, row0, p.nco_inc);
+  if (p.hist != nullptr && (int64_t)S0 + p.in_off < 0) {
+    // a streaming call's first tile, which reaches into the stream's history: sample by sample (stream_sample's
+    // rule; samples before the call's first window read as zero), 8 rows of loads in flight
+    constexpr int B = 8;
+    const InT* __restrict__ hist = reinterpret_cast<const InT*>(p.hist);
+    for (uint32_t g0 = 0; g0 < NG; g0 += B * WG) {
+      InT v[B][G];
+#pragma unroll
+      for (int b = 0; b < B; ++b) {
+        const uint32_t g = g0 + (uint32_t)b * WG + tid;
+#pragma unroll
+        for (int c = 0; c < G; ++c) {
+          const uint64_t s = S0 + (uint64_t)g * G + (uint64_t)c;
+          const int64_t i = (int64_t)s + p.in_off;
+          if (g < NG && s < p.L) {
+            v[b][c] = i < 0 ? hist[(int64_t)p.hist_len + i] : in[s];
+          } else {
+            set_zero(v[b][c]);
+          }
+        }
+      }
+#pragma unroll
+      for (int b = 0; b < B; ++b) {
+        const uint32_t g = g0 + (uint32_t)b * WG + tid;
+        if (g0 + (uint32_t)b * WG > 0) e = cmul(e, F);
+        if (g >= NG) break;
+        const float2 a = to_lds_sample(v[b][0]), c = to_lds_sample(v[b][1]);
+        lds[Geo::padded(g)] = rel_mix(make_float4(a.x, a.y, c.x, c.y), e, w);
+      }
+    }
+    return;
+  }
+  if constexpr (SH != 0) {
+    static_assert(!VEC && SH == 1, "shifted staging is for 8-byte-aligned complex or 2-byte-aligned int8 I/Q input");
+    if ((int64_t)S0 + p.in_off >= 1 && S0 + (uint64_t)NG * G <= p.L) {
+      // loaded pair g holds samples 2g - 1 (the odd half of granule g - 1: lane tid - 1's chain, or for lane 0
+      // lane WG - 1's chain one row behind) and 2g (granule g): the previous lane's chain runs beside this one
+      const uint32_t lp = (tid + WG - 1) % WG;
+      const bool lag = tid == 0 && row0 == 0;  // lane 0 of a cell's first row has no previous granule in the cell
+      float2 ep = nco_direct((2u * lp) * p.nco_inc);
+      for (uint32_t i = 0; i < row0; ++i) {
+        const float2 t = cmul(ep, F);
+        ep = (tid == 0 && i == 0) ? ep : t;  // lane 0 follows lane WG - 1 one row behind
+      }
+      float2* __restrict__ l2 = reinterpret_cast<float2*>(lds);
+#pragma unroll
+      for (int b0 = 0; b0 < BPT; b0 += SB) {
+        float4 v[SB];
+        if constexpr (std::is_same<InT, Iq8>::value) {
+          const uint32_t* __restrict__ src = reinterpret_cast<const uint32_t*>(in + S0 - 1);  // 4-byte aligned
+          uint32_t wd[SB];
+#pragma unroll
+          for (int k = 0; k < SB; ++k) {
+            wd[k] = NT ? __builtin_nontemporal_load(src + (b0 + k) * WG + tid) : src[(b0 + k) * WG + tid];
+          }
+#pragma unroll
+          for (int k = 0; k < SB; ++k) v[k] = iq8x2_granule(wd[k]);
+        } else {
+          const float4* __restrict__ src = reinterpret_cast<const float4*>(in + S0 - 1);  // 16-byte aligned
+#pragma unroll
+          for (int k = 0; k < SB; ++k) v[k] = NT ? load16_nt(src + (b0 + k) * WG + tid) : src[(b0 + k) * WG + tid];
+        }
+#pragma unroll
+        for (int k = 0; k < SB; ++k) {
+          const int row = b0 + k;
+          const uint32_t g = (uint32_t)row * WG + tid;
+          if (row > 0) {
+            e = cmul(e, F);
+            const float2 t = cmul(ep, F);
+            ep = (row == 1 && lag) ? ep : t;
+          }
+          const float2 a = cmul(make_float2(v[k].x, v[k].y), cmul(ep, w));  // sample 2g - 1
+          const float2 b = cmul(make_float2(v[k].z, v[k].w), e);            // sample 2g
+          if (g > 0) l2[2 * Geo::padded(g - 1) + 1] = a;
+          l2[2 * Geo::padded(g)] = b;
+        }
+      }
+      // the halo (its first granule rewrites the body's last slot whole): granule g of this loop is lane tid - 1's
+      // (lane 0: lane WG - 1's, one row back), i.e. the previous-lane chain's
+      for (uint32_t g = BPT * WG - 1 + tid; g < NG; g += WG) {
+        ep = cmul(ep, F);
+        lds[Geo::padded(g)] = rel_mix(load_granule<InT, false>(in, S0 + (uint64_t)g * G, p.L), ep, w);
+      }
+      return;
+    }
+  }
+  // wave-uniform: is the whole staged span readable? (not the first tile of a call starting inside its cell, not
+  // the last)
+  const bool whole = VEC && (int64_t)S0 >= 0 && (S0 + (uint64_t)NG * G <= p.L);
+  const uint32_t pbase = Geo::padded(tid);
+#pragma unroll
+  for (int b0 = 0; b0 < BPT; b0 += SB) {
+    float4 v[SB];
+    if (whole) {
+      if constexpr (std::is_same<InT, Iq8>::value) {
+        const uint32_t* __restrict__ src = reinterpret_cast<const uint32_t*>(in + S0);
+        uint32_t wd[SB];
+#pragma unroll
+        for (int k = 0; k < SB; ++k) {
+          wd[k] = NT ? __builtin_nontemporal_load(src + (b0 + k) * WG + tid) : src[(b0 + k) * WG + tid];
+        }
+#pragma unroll
+        for (int k = 0; k < SB; ++k) v[k] = iq8x2_granule(wd[k]);
+      } else {
+        const float4* __restrict__ src = reinterpret_cast<const float4*>(in + S0);
+#pragma unroll
+        for (int k = 0; k < SB; ++k) v[k] = NT ? load16_nt(src + (b0 + k) * WG + tid) : src[(b0 + k) * WG + tid];
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < SB; ++k) {
+        v[k] = load_granule<InT, VEC>(in, S0 + (uint64_t)((b0 + k) * WG + tid) * G, p.L);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < SB; ++k) {
+      if (b0 + k > 0) e = cmul(e, F);
+      const uint32_t g = (b0 + k) * WG + tid;
+      const uint32_t slot = (WG % Geo::SG == 0) ? pbase + (uint32_t)(b0 + k) * Geo::padded(WG) : Geo::padded(g);
+      lds[slot] = rel_mix(v[k], e, w);
+    }
+  }
+  for (uint32_t g = BPT * WG + tid; g < NG; g += WG) {
+    e = cmul(e, F);
+    lds[Geo::padded(g)] = rel_mix(load_granule<InT, VEC>(in, S0 + (uint64_t)g * G, p.L), e, w);
   }
 }
 
@@ -865,7 +1005,10 @@ __device__ __forceinline__ bool store_tile_lds(float4* lds, const FirParams& p, 
 
 // Shared by the tiled kernels. `xs` is a WG-sized LDS exchange area (FM mode only); `tile` the staged
 // input tile, which FM mode with COAL reuses (WG * R floats) once every wave is done with it.
-template <int MODE, class OutT, int R, int WG, bool NTS = false, bool COAL = false>
+// ANCH (anchored FM tiles, stage_tile_rel): tiles do not overlap and all KT discriminator outputs are written; a
+// thread whose last output's partner starts an FMB-output block takes that partner from xs[WG + b - 1]
+// (fm_block_outputs), every other thread from its neighbour's first output.
+template <int MODE, class OutT, int R, int WG, bool NTS = false, bool COAL = false, bool ANCH = false, int FMB = 1>
 __device__ __forceinline__ void tile_epilogue(const FirParams& p, uint64_t out0, OutT (&acc)[R], float2* xs,
                                               float4* tile = nullptr) {
   const uint32_t t = threadIdx.x;
@@ -886,8 +1029,14 @@ __device__ __forceinline__ void tile_epilogue(const FirParams& p, uint64_t out0,
     __syncthreads();
     // value select (both loads in range): a select of the two addresses became a flat load through
     // scratch when R = 1
-    const float2 nb = xs[t + 1 < WG ? t + 1 : t];
-    const float2 nxt = (t + 1 < WG) ? nb : acc[R - 1];
+    float2 nxt;
+    if constexpr (ANCH) {
+      const uint32_t tb = (t + 1) * R;  // tile-local index of the partner
+      nxt = xs[(tb % FMB) == 0 ? WG + tb / FMB - 1 : t + 1];
+    } else {
+      const float2 nb = xs[t + 1 < WG ? t + 1 : t];
+      nxt = (t + 1 < WG) ? nb : acc[R - 1];
+    }
     float o[R];
 #pragma unroll
     for (int r = 0; r + 1 < R; r += 2) {
@@ -1103,26 +1252,60 @@ __device__ __forceinline__ uint32_t tile_of_block() {
   }
 }
 
-// One tile of the polyphase kernel (the body of k_fir_poly and of k_fir_poly_grouped).
+// Anchored FM tiles: the discriminator partner of an output whose successor starts an FMB-output block. Blocks
+// of FMB outputs (the decimation's smallest tile: 256 at D = 4) tile every tile shape and every NCO cell, and the
+// partner at a block start b FMB is always formed this one way -- in the NCO frame of the output it pairs with,
+// by the wave whose outputs end there, lane-strided over the taps and then a fixed butterfly -- whether it is
+// the next tile's first output, the next cell's, or an output inside this tile; every other partner is the
+// poly core's own output. So a discriminator output is the same value in every tile shape, call split and
+// channel grouping. The products are exactly the reference's (taps below T only). Slot b - 1 of xe.
+template <class TapT, class InT, class Geo, int D, int R, int WG, int FMB>
+__device__ __forceinline__ void fm_block_outputs(const float4* __restrict__ lds, const FirParams& p, float2* xe) {
+  static_assert(FMB % R == 0 && (Geo::KT % FMB) == 0, "blocks of whole threads, whole blocks a tile");
+  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  const uint32_t tb = (64u * wv + 64u) * R;  // partner index of the wave's last output
+  if (tb % FMB != 0) return;                 // (wave-uniform)
+  const TapT* __restrict__ taps = reinterpret_cast<const TapT*>(p.taps);
+  typename Product<TapT, InT>::type a;
+  set_zero(a);
+  for (uint32_t i = lane; i < p.T; i += 64) mac(a, tile_sample<InT, Geo, true>(lds, tb * D + i), taps[i]);
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    a.x += __shfl_xor(a.x, m);
+    a.y += __shfl_xor(a.y, m);
+  }
+  if (lane == 0) xe[tb / FMB - 1] = a;
+}
+
+// One tile of the polyphase kernel (the body of k_fir_poly and of k_fir_poly_grouped). FM / AM tiles are
+// anchored (stage_tile_rel): tile t covers outputs [t KT - tile_shift, (t + 1) KT - tile_shift) and is sub-tile
+// (cell_sub0 + t) mod SUBS of its NCO cell of SUBS tiles.
 template <class TapT, class InT, int D, int R, int JC, int WG, bool VEC, int MODE, int ABL, bool NT, int CST, bool DMA,
-          int SH>
+          int SH, int SUBS = 1, int FMB = 0>
 __device__ __forceinline__ void fir_poly_tile(const FirParams& p, uint32_t tile) {
   using Geo = TileGeo<InT, D, R, WG>;
   using OutT = typename Product<TapT, InT>::type;
   constexpr int G = Geo::G;
+  constexpr bool ANCH = MODE != kModeFir;
+  constexpr int BPT = Geo::SG * (Geo::KT / Geo::ROUT) / WG;  // granule rows of the tile body
 
   extern __shared__ __attribute__((aligned(16))) float4 lds[];
   const InT* __restrict__ in = reinterpret_cast<const InT*>(p.in);
   const HistSample<InT> hist = stream_history_load<InT>(p);
 
-  const uint64_t out0 = (uint64_t)tile * p.tile_stride;
+  // (an anchored call's first tile may start before output 0: out0 and S0 are then "negative", wrapped)
+  const uint64_t out0 = ANCH ? (uint64_t)tile * Geo::KT - p.tile_shift : (uint64_t)tile * p.tile_stride;
   const uint64_t S0 = out0 * D;
   const uint32_t span = p.nch * JC * D;
-  const uint32_t NG = ((Geo::KT - 1) * D + span + G - 1) / G;
-  // LDS: [tile granules | FM exchange (WG float2)]
+  const uint32_t NG = ((MODE == kModeFm ? Geo::KT : Geo::KT - 1) * D + span + G - 1) / G;
+  // LDS: [tile granules | FM exchange (WG float2) | FM block partners (<= 4 float2)]
   constexpr int SMODE = (ABL & 8) ? (int)kModeFir : MODE;
   if constexpr ((ABL & 7) != 2) {
-    stage_tile<InT, Geo, WG, VEC, SMODE, NT, DMA, SH, (ABL & 32) != 0, (ABL & 128) != 0>(lds, in, S0, NG, p);
+    if constexpr (ANCH && SMODE != kModeFir) {
+      stage_tile_rel<InT, Geo, WG, VEC, NT, SH>(lds, in, S0, NG, p, ((p.cell_sub0 + tile) % SUBS) * BPT);
+    } else {
+      stage_tile<InT, Geo, WG, VEC, SMODE, NT, DMA, SH>(lds, in, S0, NG, p);
+    }
   }
   __syncthreads();
   stream_history_store<InT>(p, hist);
@@ -1136,10 +1319,13 @@ __device__ __forceinline__ void fir_poly_tile(const FirParams& p, uint32_t tile)
     for (int r = 0; r < R; ++r) mac(acc[r], granule_sample<typename LdsSample<InT>::type>(v, r % G), 1.0f);
   } else {
     poly_compute<TapT, InT, D, R, JC, WG, (ABL & 64) != 0>(lds, p, acc);
-    if constexpr ((ABL & ~128) == 0) {
+    if constexpr (ABL == 0) {
       if (!all_finite(acc)) poly_fixup<TapT, InT, D, R, JC, WG>(lds, p, acc);
     }
   }
+  float2* xs = reinterpret_cast<float2*>(lds + Geo::padded(NG - 1) + 1);
+  constexpr int XB = FMB > 0 ? FMB : Geo::KT;  // FM partner blocks (fm_block_outputs)
+  if constexpr (MODE == kModeFm) fm_block_outputs<TapT, InT, Geo, D, R, WG, XB>(lds, p, xs + WG);
 
   if constexpr (CST != 0 && MODE == kModeFir) {
     if (store_tile_lds<CST, OutT, R, WG>(lds, p, out0, acc)) return;
@@ -1153,89 +1339,13 @@ __device__ __forceinline__ void fir_poly_tile(const FirParams& p, uint32_t tile)
     }
     return;
   }
-  float2* xs = reinterpret_cast<float2*>(lds + Geo::padded(NG - 1) + 1);
-  tile_epilogue<MODE, OutT, R, WG, NT, true>(p, out0, acc, xs, lds);
+  tile_epilogue<MODE, OutT, R, WG, NT, true, ANCH, XB>(p, out0, acc, xs, lds);
 }
 
 template <class TapT, class InT, int D, int R, int JC, int WG, bool VEC, int MODE, int ABL = 0, bool NT = false,
-          bool XM = false, int CST = 0, bool DMA = false, int SH = 0>
+          bool XM = false, int CST = 0, bool DMA = false, int SH = 0, int SUBS = 1, int FMB = 0>
 __global__ __launch_bounds__(WG) void k_fir_poly(FirParams p) {
-  fir_poly_tile<TapT, InT, D, R, JC, WG, VEC, MODE, ABL, NT, CST, DMA, SH>(p, tile_of_block<XM>());
-}
-
-// ------------------------------------------------------------------------------------------------
-// Kernel 1p (tuning probe): FM / AM chain on persistent workgroups whose NCO phasors are tile-relative
-// and held in registers: granule k * WG + tid of every tile starts at tile-relative sample
-// G (k WG + tid), so its two phasors are the same for every tile and are computed once per workgroup.
-// The discriminator and the envelope are invariant to the rotation this leaves common to a tile.
-// ------------------------------------------------------------------------------------------------
-template <class TapT, class InT, int D, int R, int JC, int WG, int MODE>
-__global__ __launch_bounds__(WG) void k_fir_poly_rel(FirParams p, uint32_t ntiles) {
-  using Geo = TileGeo<InT, D, R, WG>;
-  using OutT = typename Product<TapT, InT>::type;
-  constexpr int G = Geo::G;
-  static_assert(G == 2 && MODE != kModeFir, "complex chains");
-  constexpr int BPT = Geo::SG * (Geo::KT / Geo::ROUT) / WG;
-  extern __shared__ __attribute__((aligned(16))) float4 lds[];
-  const InT* __restrict__ in = reinterpret_cast<const InT*>(p.in);
-  const uint32_t span = p.nch * JC * D;
-  const uint32_t NG = ((Geo::KT - 1) * D + span + G - 1) / G;
-  const uint32_t tid = threadIdx.x;
-  const uint32_t pbase = Geo::padded(tid);
-  float4 ph[BPT + 1];
-#pragma unroll
-  for (int k = 0; k <= BPT; ++k) {
-    const uint32_t s = (uint32_t)G * ((uint32_t)k * WG + tid);
-    const float2 a = nco_direct(s * p.nco_inc), b = nco_direct((s + 1u) * p.nco_inc);
-    ph[k] = make_float4(a.x, a.y, b.x, b.y);
-  }
-  for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    __syncthreads();  // the previous tile's epilogue is done with LDS
-    const uint64_t out0 = (uint64_t)tile * p.tile_stride;
-    const uint64_t S0 = out0 * D;
-    const bool whole = S0 + (uint64_t)NG * G <= p.L;
-    float4 v[BPT + 1];
-    const float4* __restrict__ src = reinterpret_cast<const float4*>(in + S0);
-    const uint32_t gh = BPT * WG + tid;
-    if (whole) {
-#pragma unroll
-      for (int k = 0; k < BPT; ++k) v[k] = load16_nt(src + k * WG + tid);
-      if (gh < NG) v[BPT] = load16_nt(src + gh);
-    } else {
-#pragma unroll
-      for (int k = 0; k < BPT; ++k) v[k] = load_granule<InT, false>(in, S0 + (uint64_t)(k * WG + tid) * G, p.L);
-      if (gh < NG) v[BPT] = load_granule<InT, false>(in, S0 + (uint64_t)gh * G, p.L);
-    }
-#pragma unroll
-    for (int k = 0; k < BPT; ++k) {
-      const float2 a = cmul(make_float2(v[k].x, v[k].y), make_float2(ph[k].x, ph[k].y));
-      const float2 b = cmul(make_float2(v[k].z, v[k].w), make_float2(ph[k].z, ph[k].w));
-      lds[pbase + (uint32_t)k * Geo::padded(WG)] = make_float4(a.x, a.y, b.x, b.y);
-    }
-    if (gh < NG) {
-      const float2 a = cmul(make_float2(v[BPT].x, v[BPT].y), make_float2(ph[BPT].x, ph[BPT].y));
-      const float2 b = cmul(make_float2(v[BPT].z, v[BPT].w), make_float2(ph[BPT].z, ph[BPT].w));
-      lds[Geo::padded(gh)] = make_float4(a.x, a.y, b.x, b.y);
-    }
-    for (uint32_t g = gh + WG; g < NG; g += WG) {  // halo beyond one row of granules (large tap counts)
-      const float4 w = load_granule<InT, false>(in, S0 + (uint64_t)g * G, p.L);
-      const float2 a = cmul(make_float2(w.x, w.y), nco_direct((uint32_t)G * g * p.nco_inc));
-      const float2 b = cmul(make_float2(w.z, w.w), nco_direct(((uint32_t)G * g + 1u) * p.nco_inc));
-      lds[Geo::padded(g)] = make_float4(a.x, a.y, b.x, b.y);
-    }
-    __syncthreads();
-    OutT acc[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) set_zero(acc[r]);
-    // the taps are loop-invariant: hoisted out of the tile loop they held ~128 VGPRs (they do not fit
-    // the SGPRs), so their address is made opaque per tile and the scalar loads stay in the core
-    FirParams pt = p;
-    asm volatile("" : "+s"(pt.taps));
-    poly_compute<TapT, InT, D, R, JC, WG, false, true>(lds, pt, acc);
-    if (!all_finite(acc)) poly_fixup<TapT, InT, D, R, JC, WG>(lds, pt, acc);
-    float2* xs = reinterpret_cast<float2*>(lds + Geo::padded(NG - 1) + 1);
-    tile_epilogue<MODE, OutT, R, WG, true, true>(p, out0, acc, xs, lds);
-  }
+  fir_poly_tile<TapT, InT, D, R, JC, WG, VEC, MODE, ABL, NT, CST, DMA, SH, SUBS, FMB>(p, tile_of_block<XM>());
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1259,7 +1369,7 @@ struct MultiParams {
 // channel c is bit-identical to gsdrFmDemod / gsdrAmDemod with its own frequency by construction, at
 // the single-channel kernel's register budget. (The first multi-channel kernel read each input tile
 // into registers once and looped over the channels: 228 VGPRs, 2 waves per SIMD, 5 % slower.)
-template <class TapT, class InT, int D, int R, int JC, int WG, bool VEC, int MODE, int SH = 0>
+template <class TapT, class InT, int D, int R, int JC, int WG, bool VEC, int MODE, int SH = 0, int FMB = 0>
 __global__ __launch_bounds__(WG) void k_fir_poly_grouped(FirParams p, MultiParams mp, uint32_t tiles) {
   const uint32_t C = mp.count;
   const uint32_t b = blockIdx.x, r = b >> 3;
@@ -1270,7 +1380,7 @@ __global__ __launch_bounds__(WG) void k_fir_poly_grouped(FirParams p, MultiParam
   pc.fm_gain = mp.gain[c];
   pc.out = reinterpret_cast<float*>(p.out) + (uint64_t)c * mp.out_stride;
   if (c != 0) pc.hist_out = nullptr;  // a multi-channel stream step: channel 0's workgroup 0 copies the history
-  fir_poly_tile<TapT, InT, D, R, JC, WG, VEC, MODE, 0, true, 0, false, SH>(pc, tile);
+  fir_poly_tile<TapT, InT, D, R, JC, WG, VEC, MODE, 0, true, 0, false, SH, 1, FMB>(pc, tile);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1609,12 +1719,14 @@ constexpr size_t mfma_bc_lds_bytes(uint32_t T) {
 // ------------------------------------------------------------------------------------------------
 // Host-side sizing helpers
 // ------------------------------------------------------------------------------------------------
+// (FM: the tile also holds the window of FIR output KT and the exchange area the block partners of the anchored
+// polyphase tiles, fm_block_outputs; the contiguous-window kernels use less)
 template <class InT, int D, int R, int WG>
 constexpr size_t poly_lds_bytes(uint32_t span_samples, int mode) {
   using Geo = TileGeo<InT, D, R, WG>;
-  const uint32_t NG = ((Geo::KT - 1) * D + span_samples + Geo::G - 1) / Geo::G;
+  const uint32_t NG = ((mode == kModeFm ? Geo::KT : Geo::KT - 1) * D + span_samples + Geo::G - 1) / Geo::G;
   size_t bytes = (size_t)(Geo::padded(NG - 1) + 1) * 16u;
-  if (mode != kModeFir) bytes += ((size_t)WG * sizeof(float2) + 15) / 16 * 16;
+  if (mode != kModeFir) bytes += ((size_t)(WG + 4) * sizeof(float2) + 15) / 16 * 16;
   return bytes;
 }
 

@@ -52,6 +52,7 @@ static hipError_t chain_entry(int mode, float fs, float tune, float chan, float 
   // the int8 matrix-core chains align their 16-output blocks to the absolute output index
   // firstSampleIndex / D + k, so chunked calls reproduce one call bit for bit (fir_i8_mfma.hpp)
   job.out_phase = (uint32_t)((firstSampleIndex / decimation) & 15u);
+  job.q0 = (uint32_t)(firstSampleIndex / decimation);  // the anchored tiles' NCO cell grid
   if (mode == kModeFm) {
     job.L = numOutputs * (size_t)decimation + tapCount;  // N + 1 FIR outputs
     job.fm_gain = fs / (2.0f * kPiF * dev);              // as reference src/fm.cu:203
@@ -105,6 +106,7 @@ static hipError_t chain_multi_entry(int mode, float fs, float tune, const float*
       job.N = numOutputs;
       job.mode = mode;
       job.nco_n0 = (uint32_t)firstSampleIndex;
+      job.q0 = (uint32_t)(firstSampleIndex / decimation);
       job.L = mode == kModeFm ? numOutputs * (size_t)decimation + tapCount
                               : (numOutputs - 1) * (size_t)decimation + tapCount;
       DeviceScope scope(device);
@@ -149,6 +151,7 @@ hipError_t chain_int8_stream_step(int mode, float fs, float tune, float chan, fl
   job.mode = mode;
   job.nco_n0 = (uint32_t)firstSampleIndex;
   job.out_phase = (uint32_t)((firstSampleIndex / 4) & 15u);
+  job.q0 = (uint32_t)(firstSampleIndex / 4);
   if (mode == kModeFm) job.fm_gain = fs / (2.0f * kPiF * dev);
   job.in_off = inOff;
   job.hist = hist;
@@ -179,6 +182,7 @@ hipError_t chain_stream_step_tiled(int mode, bool int8, float fs, float tune, fl
   job.L = chunkLen;
   job.mode = mode;
   job.nco_n0 = (uint32_t)firstSampleIndex;
+  job.q0 = (uint32_t)(firstSampleIndex / decimation);
   if (mode == kModeFm) job.fm_gain = fs / (2.0f * kPiF * dev);
   job.in_off = inOff;
   job.hist = hist;
@@ -233,6 +237,7 @@ hipError_t chain_multi_stream_step(int mode, float fs, float tune, const float* 
     job.N = numOutputs;
     job.mode = mode;
     job.nco_n0 = (uint32_t)firstSampleIndex;
+    job.q0 = (uint32_t)(firstSampleIndex / decimation);
     job.in_off = inOff;
     job.hist = hist;
     job.hist_len = histLen;

@@ -26,7 +26,6 @@
 
 
 #include <algorithm>
-#include <atomic>
 
 #include "gsdr/iir.h"
 #include "launch.hpp"
@@ -768,15 +767,22 @@ __global__ __launch_bounds__(64 * kUpperWaves) void k_iir_scan_upper(uint64_t E1
   }
 }
 
+// Which formulation a call runs: the multi-pass scan below (the product's only path), or -- in the tuning-probe
+// build only -- the single-pass kernel of iir_resident.hpp, chosen per call (gsdrxIirFFSinglePass / CC).
+struct PathSel {
+  bool single_pass = false;
+  uint32_t max_polls = 0;  // the single-pass kernel's bound on every wait
+};
+
+#ifdef GSDR_TUNING_PROBES
 #include "iir_resident.hpp"
 
-std::atomic<int> g_single_pass{0};
-
-// A per-call epoch for the single-pass kernel's flags (never repeats within the process; seeded from the clock
-// and the process id so stale flags of another process's allocations cannot match either).
+// bit 0: a single-pass tile gave up waiting since the last gsdrxIirSinglePassStatus (per device)
+__device__ uint32_t g_res_status;
 
 template <class S, int P>
-static hipError_t run_resident(const Coeffs& cf, S* xh, S* yh, const S* x, S* y, uint64_t n, hipStream_t st) {
+static hipError_t run_resident(const Coeffs& cf, S* xh, S* yh, const S* x, S* y, uint64_t n, hipStream_t st,
+                               uint32_t max_polls) {
   using Sh = res::Shape<S>;
   constexpr int NC = Sh::NC;
   const uint64_t ntiles = ceil_div<uint64_t>(n, Sh::TS);
@@ -785,7 +791,11 @@ static hipError_t run_resident(const Coeffs& cf, S* xh, S* yh, const S* x, S* y,
   // kernel), the tables and coefficients
   const uint64_t nagg = (ntiles + nsb) * P * NC;
   const size_t off_tabs = nagg * sizeof(double);
-  const size_t bytes = off_tabs + (res::res_tab_doubles<P>() + res::res_coef_doubles<P>()) * sizeof(double);
+  const size_t off_ticket = off_tabs + (res::res_tab_doubles<P>() + res::res_coef_doubles<P>()) * sizeof(double);
+  const size_t bytes = off_ticket + 16;
+  void* status = nullptr;
+  hipError_t se = hipGetSymbolAddress(&status, HIP_SYMBOL(g_res_status));
+  if (se != hipSuccess) return se;
   char* ws = nullptr;
   hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&ws), bytes, st);
   if (e != hipSuccess) return e;
@@ -797,9 +807,12 @@ static hipError_t run_resident(const Coeffs& cf, S* xh, S* yh, const S* x, S* y,
   ra.xh_out = reinterpret_cast<float*>(xh);
   ra.yh_out = reinterpret_cast<float*>(yh);
   ra.Pk = cf.K - 1;
+  ra.ticket = reinterpret_cast<uint32_t*>(ws + off_ticket);
+  ra.status = static_cast<uint32_t*>(status);
+  ra.max_polls = max_polls;
   const bool vec = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15u) == 0;
   const uint32_t nclear = (uint32_t)std::min<uint64_t>(512, ceil_div<uint64_t>(nagg, 8 * res::kResWG));
-  res::k_res_setup<S, P><<<1 + nclear, res::kResWG, 0, st>>>(cf, tabs, reinterpret_cast<uint64_t*>(ws), nagg);
+  res::k_res_setup<S, P><<<1 + nclear, res::kResWG, 0, st>>>(cf, tabs, reinterpret_cast<uint64_t*>(ws), nagg, ra.ticket);
   if (vec) {
     res::k_iir_resident<S, P, true><<<(uint32_t)ntiles, res::kResWG, 0, st>>>(cf, x, xh, yh, n, y, ra);
   } else {
@@ -810,15 +823,19 @@ static hipError_t run_resident(const Coeffs& cf, S* xh, S* yh, const S* x, S* y,
   return e != hipSuccess ? e : f;
 }
 
+#endif  // GSDR_TUNING_PROBES
+
 template <class S, int P>
-static hipError_t run(const Coeffs& cf, S* xh, S* yh, const S* x, S* y, uint64_t n, hipStream_t st) {
-  // K <= 9 and up to 2^16 tiles (2^29 real / 2^28 complex samples), when selected (gsdrxIirSetSinglePass):
-  // the single-pass kernel. Measured slower than the scan below on MI355X, so off by
-  // default.
-  if constexpr (P <= kFusedMaxP) {
-    if (g_single_pass.load(std::memory_order_relaxed) &&
-        ceil_div<uint64_t>(n, res::Shape<S>::TS) <= res::kResMaxTiles)
-      return run_resident<S, P>(cf, xh, yh, x, y, n, st);
+static hipError_t run(const Coeffs& cf, S* xh, S* yh, const S* x, S* y, uint64_t n, hipStream_t st, PathSel ps) {
+  if (ps.single_pass) {
+#ifdef GSDR_TUNING_PROBES
+    // K <= 9 and up to 2^16 tiles (2^29 real / 2^28 complex samples); anything else is refused, not rerouted
+    if constexpr (P <= kFusedMaxP) {
+      if (ceil_div<uint64_t>(n, res::Shape<S>::TS) <= res::kResMaxTiles)
+        return run_resident<S, P>(cf, xh, yh, x, y, n, st, ps.max_polls);
+    }
+#endif
+    return hipErrorNotSupported;
   }
   using A = typename Acc<S>::type;
   const uint64_t C = ceil_div<uint64_t>(n, kChunk);
@@ -931,7 +948,7 @@ static hipError_t run(const Coeffs& cf, S* xh, S* yh, const S* x, S* y, uint64_t
 
 template <class S>
 static hipError_t entry(const float* b, const float* a, size_t K, S* xh, S* yh, const S* x, S* y, size_t n,
-                        int32_t device, hipStream_t st) {
+                        int32_t device, hipStream_t st, PathSel ps = {}) {
   if (K < 2 || K > 32) return hipErrorInvalidValue;  // reference limits (iir.cu:229-235)
   if (n == 0) return hipSuccess;
   if (b == nullptr || a == nullptr || x == nullptr || y == nullptr) return hipErrorInvalidValue;
@@ -940,12 +957,12 @@ static hipError_t entry(const float* b, const float* a, size_t K, S* xh, S* yh, 
   if (scope.status() != hipSuccess) return scope.status();
   const Coeffs cf{b, a, (int)K};
   const size_t P = K - 1;
-  if (P <= 1) return run<S, 1>(cf, xh, yh, x, y, n, st);
-  if (P <= 2) return run<S, 2>(cf, xh, yh, x, y, n, st);
-  if (P <= 4) return run<S, 4>(cf, xh, yh, x, y, n, st);
-  if (P <= 8) return run<S, 8>(cf, xh, yh, x, y, n, st);
-  if (P <= 16) return run<S, 16>(cf, xh, yh, x, y, n, st);
-  return run<S, 31>(cf, xh, yh, x, y, n, st);
+  if (P <= 1) return run<S, 1>(cf, xh, yh, x, y, n, st, ps);
+  if (P <= 2) return run<S, 2>(cf, xh, yh, x, y, n, st, ps);
+  if (P <= 4) return run<S, 4>(cf, xh, yh, x, y, n, st, ps);
+  if (P <= 8) return run<S, 8>(cf, xh, yh, x, y, n, st, ps);
+  if (P <= 16) return run<S, 16>(cf, xh, yh, x, y, n, st, ps);
+  return run<S, 31>(cf, xh, yh, x, y, n, st, ps);
 }
 
 }  // namespace iir
@@ -986,6 +1003,48 @@ GSDR_C_LINKAGE hipError_t gsdrIirCCCustom(const float* bCoeffs, const float* aCo
                    cudaStream);
 }
 
-GSDR_C_LINKAGE int gsdrxIirSetSinglePass(int enable) GSDR_NO_EXCEPT {
-  return gsdr::iir::g_single_pass.exchange(enable != 0 ? 1 : 0);
+#ifdef GSDR_TUNING_PROBES
+// Tuning-probe build only (libgsdr_probes.so; tools/ and tests/test_gpu_iir_single_pass.py bind them by name):
+// gsdrIirFF / gsdrIirCC on the single-pass kernel, chosen per call. maxPolls bounds every wait in polling rounds
+// (2^22 is the measured setting; 0 makes every tile that has to wait give up at once, which is how the status
+// path is tested); hipErrorNotSupported for K > 9 or more than 2^16 tiles. A give-up is reported by
+// gsdrxIirSinglePassStatus, which synchronises the stream and returns hipErrorLaunchFailure (clearing the word)
+// when any tile gave up since the last query.
+#define GSDR_PROBE_API extern "C" __attribute__((visibility("default")))
+GSDR_PROBE_API hipError_t gsdrxIirFFSinglePass(const float* bCoeffs, const float* aCoeffs, size_t coeffCount,
+                                               float* inputHistory, float* outputHistory, const float* input,
+                                               float* output, size_t numElements, uint32_t maxPolls,
+                                               int32_t cudaDevice, hipStream_t cudaStream) noexcept {
+  return gsdr::iir::entry<float>(bCoeffs, aCoeffs, coeffCount, inputHistory, outputHistory, input, output,
+                                 numElements, cudaDevice, cudaStream,
+                                 gsdr::iir::PathSel{true, maxPolls});
 }
+
+GSDR_PROBE_API hipError_t gsdrxIirCCSinglePass(const float* bCoeffs, const float* aCoeffs, size_t coeffCount,
+                                               hipFloatComplex* inputHistory, hipFloatComplex* outputHistory,
+                                               const hipFloatComplex* input, hipFloatComplex* output,
+                                               size_t numElements, uint32_t maxPolls, int32_t cudaDevice,
+                                               hipStream_t cudaStream) noexcept {
+  return gsdr::iir::entry<float2>(bCoeffs, aCoeffs, coeffCount, reinterpret_cast<float2*>(inputHistory),
+                                  reinterpret_cast<float2*>(outputHistory), reinterpret_cast<const float2*>(input),
+                                  reinterpret_cast<float2*>(output), numElements, cudaDevice, cudaStream,
+                                  gsdr::iir::PathSel{true, maxPolls});
+}
+
+// hipSuccess when no single-pass tile gave up since the last query, else hipErrorLaunchFailure
+GSDR_PROBE_API hipError_t gsdrxIirSinglePassStatus(int32_t cudaDevice, hipStream_t cudaStream) noexcept {
+  gsdr::DeviceScope scope(cudaDevice);
+  if (scope.status() != hipSuccess) return scope.status();
+  uint32_t v = 0;
+  hipError_t e = hipMemcpyFromSymbolAsync(&v, HIP_SYMBOL(gsdr::iir::g_res_status), sizeof(v), 0,
+                                          hipMemcpyDeviceToHost, cudaStream);
+  if (e == hipSuccess) e = hipStreamSynchronize(cudaStream);
+  if (e != hipSuccess) return e;
+  if (v == 0) return hipSuccess;
+  const uint32_t z = 0;
+  e = hipMemcpyToSymbolAsync(HIP_SYMBOL(gsdr::iir::g_res_status), &z, sizeof(z), 0, hipMemcpyHostToDevice,
+                             cudaStream);
+  if (e == hipSuccess) e = hipStreamSynchronize(cudaStream);
+  return e != hipSuccess ? e : hipErrorLaunchFailure;
+}
+#endif

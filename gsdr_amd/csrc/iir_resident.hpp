@@ -1,4 +1,7 @@
-// gsdr-mi355x: single-pass IIR (gsdrIirFF / gsdrIirCC for K <= 9, up to 2^16 tiles), included by iir.hip.
+// gsdr-mi355x: single-pass IIR (K <= 9, up to 2^16 tiles), included by iir.hip in the tuning-probe build only
+// (GSDR_TUNING_PROBES: gsdrxIirFFSinglePass / gsdrxIirCCSinglePass of libgsdr_probes.so). It measured slower than
+// the multi-pass scan that gsdrIirFF / gsdrIirCC run, so the product library does not
+// carry it.
 //
 // The multi-pass scan of iir.hip reads the input twice (tails pass, final pass) with scan launches between,
 // and both chunk passes are latency-bound. Here one launch reads x once and writes y
@@ -8,7 +11,7 @@
 //      floats, as iir.hip's chunk passes); each lane filters its chunk from zero output state -> its tail;
 //   2. an inclusive affine scan of the chunk tails across the workgroup (Hillis-Steele with M0^(2^s), M0 =
 //      the transition over one chunk) gives every chunk's zero-entry prefix and the tile's aggregate, which
-//      the workgroup publishes (flag = this call's epoch, so the workspace needs no clearing);
+//      the workgroup publishes (into aggregate arrays the setup kernel fills with a sentinel on every call);
 //   3. the tile's entry state: tiles are grouped in superblocks of 256; the last tile of a superblock also
 //      publishes the superblock's aggregate. A workgroup waits for the aggregates of the tiles before it in
 //      its superblock and of the superblocks before its own, scans each list across its threads (fixed
@@ -17,9 +20,11 @@
 //      (k = its index in the superblock, U / Q the inclusive scans, M_T = M0^(chunks a tile), M_SB = M_T^256);
 //   4. every chunk starts from M0^e S_tile + prefix_(e-1), the recursion re-runs over the staged tile and y leaves
 //      through LDS in coalesced rows.
-// A workgroup waits only on lower-numbered ones, which the hardware dispatches first (per XCD, in order), so
-// the waits cannot deadlock whatever the grid size; every wait is bounded (a give-up leaves NaN outputs
-// rather than a hung device). The transition matrices and their powers are built once per call by a
+// Tile numbers come from an atomic ticket taken when a workgroup starts, so a workgroup waits only on tiles
+// whose workgroups are already running: the waits cannot deadlock whatever order the hardware dispatches the
+// grid in. Every wait is bounded (ResArgs::max_polls rounds): a tile that gives up records it in the device
+// status word (gsdrxIirSinglePassStatus turns it into hipErrorLaunchFailure), writes NaN outputs and leaves
+// the caller's history buffers alone. The transition matrices and their powers are built once per call by a
 // one-workgroup kernel ahead of the tiles (k_res_setup); every tile loads them beside its samples.
 #pragma once
 
@@ -48,16 +53,19 @@ struct ResArgs {
   float* xh_out;
   float* yh_out;
   int Pk;
+  uint32_t* ticket;     // tile ticket counter (zeroed by k_res_setup)
+  uint32_t* status;     // device status word: bit 0 set by a tile that gave up waiting
+  uint32_t max_polls;   // bound on every wait's polling rounds
 };
 
 // Cross-workgroup values (the aggregates). Every XCD has its own L2, not coherent with the others, and
-// acquire / release at agent scope write back and invalidate the whole L2 of the XCD; with hundreds of polls
-// a tile that cost more than the filter. So there are no flags: the setup kernel fills the aggregate arrays
-// with kResEmpty (a signalling NaN whose low payload bits no float input or arithmetic result can carry), a
-// workgroup writes its aggregate with agent-scope atomic stores (they bypass the non-coherent caching) and
-// a reader polls the values themselves with agent-scope atomic loads until none is kResEmpty: each 8-byte
-// value is written and read whole, so no value can be seen half-written, and a write needs no fence or
-// completion wait before the writer moves on.
+// acquire / release write back and invalidate the whole L2 of the XCD; with hundreds of polls a tile that cost
+// more than the filter. So there are no flags: the setup kernel fills the aggregate arrays with kResEmpty (a
+// signalling NaN whose low payload bits no float input or arithmetic result can carry), a workgroup writes its
+// aggregate with relaxed atomic stores at GSDR_RES_SCOPE (system scope by default -- the setting every
+// measurement used; they bypass the non-coherent caching) and a reader polls the values themselves with relaxed
+// atomic loads of the same scope until none is kResEmpty: each 8-byte value is written and read whole, so no
+// value can be seen half-written, and a write needs no fence or completion wait before the writer moves on.
 constexpr uint64_t kResEmpty = 0x7FF4DEAD5EED1234ull;
 #ifndef GSDR_RES_SCOPE
 #define GSDR_RES_SCOPE __HIP_MEMORY_SCOPE_SYSTEM
@@ -67,18 +75,23 @@ __device__ __forceinline__ void st_co(double* p, double v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, GSDR_RES_SCOPE);
 }
 
-// out <- the N values at src once none is kResEmpty (all threads of a wave poll together); false after ~2^22
-// rounds (never expected: the writers are lower-numbered workgroups, dispatched earlier)
-// load one value (agent scope, bypassing the non-coherent caching)
+// load one value (GSDR_RES_SCOPE, bypassing the non-coherent caching)
 __device__ __forceinline__ uint64_t ld_bits(const double* p) {
   return __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED, GSDR_RES_SCOPE);
 }
 
-// the same for two sources at once (either may be null: nothing to wait for). Each round polls only the last
-// value of each source (one load per source while waiting), then reads them whole
+// oa / ob <- the N values at a / b once none is kResEmpty (either source may be null: nothing to wait for). Each
+// round polls only the last value of each source (one load per source while waiting), then reads them whole;
+// false after `lim` rounds (never expected: the writers are workgroups that took earlier tickets)
 template <int N>
-__device__ __forceinline__ bool poll_vals2(const double* a, double (&oa)[N], const double* b, double (&ob)[N]) {
-  for (uint32_t it = 0; it < (1u << 22); ++it) {
+__device__ __forceinline__ bool poll_vals2(const double* a, double (&oa)[N], const double* b, double (&ob)[N],
+                                           uint32_t lim) {
+  if (!a && !b) {  // nothing to wait for (whatever the bound)
+#pragma unroll
+    for (int i = 0; i < N; ++i) oa[i] = ob[i] = 0.0;
+    return true;
+  }
+  for (uint32_t it = 0; it < lim; ++it) {
     const bool ra = !a || ld_bits(a + N - 1) != kResEmpty;
     const bool rb = !b || ld_bits(b + N - 1) != kResEmpty;
     if (ra && rb) {
@@ -99,14 +112,14 @@ __device__ __forceinline__ bool poll_vals2(const double* a, double (&oa)[N], con
 
 // wave 0 waits until the last value of each of na vectors at a (and nb at b, stride N doubles, na, nb <= 256)
 // is written, then the workgroup barrier: one polling wave, so the co-resident workgroups still computing keep
-// their issue slots; false (for every thread) after ~2^22 rounds
+// their issue slots; false (for every thread) after `lim` rounds
 template <int N>
-__device__ __forceinline__ bool wave0_wait(const double* a, uint32_t na, const double* b, uint32_t nb) {
+__device__ __forceinline__ bool wave0_wait(const double* a, uint32_t na, const double* b, uint32_t nb, uint32_t lim) {
   bool ok = true;
-  if (threadIdx.x < 64) {
+  if (threadIdx.x < 64 && (na | nb) != 0) {
     const uint32_t lane = threadIdx.x;
     ok = false;
-    for (uint32_t it = 0; it < (1u << 22); ++it) {
+    for (uint32_t it = 0; it < lim; ++it) {
       bool all = true;
 #pragma unroll
       for (uint32_t r = 0; r < 4; ++r) {
@@ -125,9 +138,9 @@ __device__ __forceinline__ bool wave0_wait(const double* a, uint32_t na, const d
 }
 
 template <int N>
-__device__ __forceinline__ bool poll_vals(const double* src, double (&out)[N]) {
+__device__ __forceinline__ bool poll_vals(const double* src, double (&out)[N], uint32_t lim) {
   double dummy[N];
-  return poll_vals2<N>(src, out, nullptr, dummy);
+  return poll_vals2<N>(src, out, nullptr, dummy, lim);
 }
 
 // v <- M v (P x P row-major M in LDS or global)
@@ -246,8 +259,9 @@ constexpr int res_tab_doubles() { return kChunk * P + 25 * P * P; }
 
 template <class S, int P>
 __global__ __launch_bounds__(kResWG) void k_res_setup(Coeffs cf, double* __restrict__ tabs, uint64_t* __restrict__ agg,
-                                                     uint64_t nagg) {
+                                                     uint64_t nagg, uint32_t* __restrict__ ticket) {
   constexpr int PP = P * P;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *ticket = 0u;
   if (blockIdx.x > 0) {  // the aggregate arrays to kResEmpty
     for (uint64_t e = (uint64_t)(blockIdx.x - 1) * kResWG + threadIdx.x; e < nagg; e += (uint64_t)(gridDim.x - 1) * kResWG)
       agg[e] = kResEmpty;
@@ -330,7 +344,12 @@ __global__ __launch_bounds__(kResWG) __attribute__((amdgpu_waves_per_eu(res_wave
   GSDR_RES_TS0();
   const int comp = t % NC;
   const int lc = t / NC;  // chunk within the tile
-  const uint32_t tile_id = blockIdx.x;
+  // the tile this workgroup filters: the next ticket (not blockIdx.x), so every tile it waits for belongs to a
+  // workgroup that is already running, whatever order the grid is dispatched in
+  __shared__ uint32_t tile_sh;
+  if (t == 0) tile_sh = atomicAdd(ra.ticket, 1u);
+  __syncthreads();
+  const uint32_t tile_id = tile_sh;
   const uint64_t base = (uint64_t)tile_id * Sh::TS;
   const uint64_t ntiles = (n + Sh::TS - 1) / Sh::TS;
   const uint32_t tlen = n - base < (uint64_t)Sh::TS ? (uint32_t)(n - base) : (uint32_t)Sh::TS;
@@ -484,7 +503,7 @@ __global__ __launch_bounds__(kResWG) __attribute__((amdgpu_waves_per_eu(res_wave
   bool ok = true;
   auto poll_into = [&](const double* src, A (&v)[P]) {
     double tmp[NV2];
-    ok = poll_vals<NV2>(src, tmp) && ok;
+    ok = poll_vals<NV2>(src, tmp, ra.max_polls) && ok;
 #pragma unroll
     for (int i = 0; i < P; ++i) {
 #pragma unroll
@@ -505,10 +524,10 @@ __global__ __launch_bounds__(kResWG) __attribute__((amdgpu_waves_per_eu(res_wave
   A tot[P];
   if (!last_in_sb) {
     {
-      ok = wave0_wait<NV2>(ra.loc + (size_t)sb * kResSB * P * NC, k_in, ra.sbagg, sb);
+      ok = wave0_wait<NV2>(ra.loc + (size_t)sb * kResSB * P * NC, k_in, ra.sbagg, sb, ra.max_polls);
       double tu[NV2], tq[NV2];
       ok = poll_vals2<NV2>(u_mine ? ra.loc + (size_t)h * P * NC : nullptr, tu,
-                           q_mine ? ra.sbagg + (size_t)t * P * NC : nullptr, tq) && ok;
+                           q_mine ? ra.sbagg + (size_t)t * P * NC : nullptr, tq, ra.max_polls) && ok;
       GSDR_RES_TS(9);
 #pragma unroll
       for (int i = 0; i < P; ++i) {
@@ -529,7 +548,7 @@ __global__ __launch_bounds__(kResWG) __attribute__((amdgpu_waves_per_eu(res_wave
   } else {
     // the superblock's aggregate first: G_sb = M_T (sum_{j<255} M_T^(254-j) L_j) + L_255 (the last thread
     // holds this tile's own L, the last chunk's prefix, for NC == 1; both components' lanes for NC == 2)
-    ok = wave0_wait<NV2>(ra.loc + (size_t)sb * kResSB * P * NC, k_in, nullptr, 0);
+    ok = wave0_wait<NV2>(ra.loc + (size_t)sb * kResSB * P * NC, k_in, nullptr, 0, ra.max_polls);
     if (u_mine) poll_into(ra.loc + (size_t)h * P * NC, ut);
     if (u_mine) mat_pow_vec<A, P>(pwg, k_in - 1 - (uint32_t)t, ut);
     A us[P];
@@ -542,7 +561,7 @@ __global__ __launch_bounds__(kResWG) __attribute__((amdgpu_waves_per_eu(res_wave
 #pragma unroll
       for (int i = 0; i < P; ++i) st_co(ra.sbagg + ((size_t)sb * P + i) * NC + comp, g[i] + pfx[i]);
     }
-    ok = wave0_wait<NV2>(nullptr, 0, ra.sbagg, sb) && ok;
+    ok = wave0_wait<NV2>(nullptr, 0, ra.sbagg, sb, ra.max_polls) && ok;
     if (q_mine) poll_into(ra.sbagg + (size_t)t * P * NC, qt);
     q_term();
     wg_sum<A, P>(qt, tot, scA);
@@ -578,9 +597,10 @@ __global__ __launch_bounds__(kResWG) __attribute__((amdgpu_waves_per_eu(res_wave
 #pragma unroll
     for (int i = 0; i < P; ++i) st[i] += pv[i];
   }
-  if (!ok) {
+  if (!ok) {  // gave up waiting: NaN outputs, and the status word tells the host (gsdrxIirSinglePassStatus)
 #pragma unroll
     for (int i = 0; i < P; ++i) st[i] = __builtin_nan("");
+    if (t == 0) atomicOr(ra.status, 1u);
   }
   // y = y_zs + sum_i gk[k][i] st_i: the free response from the chunk's start state, added without a recursion
   {
@@ -599,7 +619,7 @@ __global__ __launch_bounds__(kResWG) __attribute__((amdgpu_waves_per_eu(res_wave
   }
   lds_barrier();
   GSDR_RES_TS(7);
-  if (len > 0 && n0 + len == n) {
+  if (len > 0 && n0 + len == n && ok) {  // (a tile that gave up may not have waited for the readers)
     // the state after the call (outputs, then inputs, newest first) into the caller's history buffers: the
     // outputs as written (from the tile; before it, the tile's entry state)
 #pragma unroll

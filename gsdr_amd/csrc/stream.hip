@@ -350,6 +350,8 @@ GSDR_C_LINKAGE hipError_t gsdrxStreamProcess(gsdrxStream s, const void* input, s
         }
       }
       if (ec == hipErrorNotSupported && c == 0) break;
+      // a failure after channel 0 leaves channels 0..c-1 written and the stream unchanged (stream.h: the
+      // outputs of a failed call are unspecified)
       if (ec != hipSuccess) {
         e = ec == hipErrorNotSupported ? hipErrorUnknown : ec;  // (one shape for every channel: cannot happen)
         break;

@@ -87,12 +87,4 @@ GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrIirCCCustom(
     int32_t cudaDevice,
     hipStream_t cudaStream) GSDR_NO_EXCEPT;
 
-/*
- * Extension (no reference counterpart): selects the single-pass IIR kernel (one launch reading x once,
- * tiles chained by look-back) for K <= 9 and up to 2^29 real / 2^28 complex samples instead of the
- * multi-pass scan. Both give results within the tests' float64 bounds; the multi-pass scan is the default
- * because it measured faster on MI355X. Process-wide; returns the previous setting.
- */
-GSDR_C_LINKAGE GSDR_PUBLIC int gsdrxIirSetSinglePass(int enable) GSDR_NO_EXCEPT;
-
 #endif /* GSDR_IIR_H_ */

@@ -110,6 +110,10 @@ GSDR_C_LINKAGE GSDR_PUBLIC size_t gsdrxStreamOutputsFor(gsdrxStream stream, size
  * `*numOutputsWritten` receives the count (host-known, no synchronisation). Asynchronous on
  * `cudaStream`; the input chunk may be reused once the stream's work has completed. Returns
  * hipErrorInvalidValue, leaving the stream unchanged, when outputCapacity is too small.
+ * On any other error (a launch failing) the stream's state is also left unchanged -- the same chunk can
+ * be passed again -- but the contents of `output` are unspecified: a multi-channel stream launches its
+ * channels (or groups of 16) in turn, and the launches before the failing one have written their
+ * channels' outputs.
  */
 GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxStreamProcess(
     gsdrxStream stream,

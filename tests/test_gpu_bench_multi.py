@@ -23,11 +23,20 @@ def free_port():
         return s.getsockname()[1]
 
 
-def test_bench_two_ranks_rehearsal(cuda):
+@pytest.mark.parametrize("launcher", ["torchrun", "plain"])
+def test_bench_two_ranks_rehearsal(cuda, launcher):
+    """launcher = torchrun: the driver's form; plain: `python bench.py --gpus 2`, which starts its own rank
+    processes (bench.self_launch) and must produce the same validated line."""
     env = dict(os.environ, BENCH_REHEARSE="1", MASTER_ADDR="127.0.0.1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--steps", "5", "--warmup", "2", "--settle-max", "50", "--no-cpu-baseline"]
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE"):
+        env.pop(k, None)
+    args = [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "5", "--warmup", "2", "--settle-max", "50",
+            "--no-cpu-baseline"]
+    if launcher == "torchrun":
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+               "--master-addr", "127.0.0.1", "--master-port", str(free_port())] + args
+    else:
+        cmd = [sys.executable] + args
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

@@ -7,6 +7,9 @@ well under e_seq32, the same measure for a plain sequential float32 loop (oracle
 reference's per-sample loop computes), which reaches 1e-4..1e-3 on the high-order filters below.
 Across calls the state travels through the caller's float32 history buffers (the reference ABI), whose
 rounding the next call's outputs inherit; that end-to-end check uses max(IIR_TOL, 4 * e_seq32)."""
+import ctypes
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -19,15 +22,61 @@ pytestmark = pytest.mark.gpu
 IIR_TOL = 1e-6
 
 
-@pytest.fixture(autouse=True, params=["scan", "single_pass"])
-def iir_kernel(request, cuda):
-    """Every test runs on both IIR paths: the multi-pass scan (default) and the single-pass kernel
-    (gsdrxIirSetSinglePass; K <= 9, larger K falls back to the scan)."""
-    from gsdr_amd import abi
+PROBES = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "build", "probes",
+                      "libgsdr_probes.so")
+HIP_ERROR_NOT_SUPPORTED, HIP_ERROR_LAUNCH_FAILURE = 801, 719
+_probes = []
 
-    prev = abi.lib.gsdrxIirSetSinglePass(1 if request.param == "single_pass" else 0)
-    yield request.param
-    abi.lib.gsdrxIirSetSinglePass(prev)
+
+def probes_lib():
+    """The tuning-probe build (make probes), which alone carries the single-pass IIR kernel; the product
+    library runs the multi-pass scan only. Missing on a GPU box = a failed test, not a skip."""
+    if not _probes:
+        assert os.path.exists(PROBES), f"{PROBES} missing (make probes)"
+        lib = ctypes.CDLL(PROBES)
+        p, sz = ctypes.c_void_p, ctypes.c_size_t
+        for name in ("gsdrxIirFFSinglePass", "gsdrxIirCCSinglePass"):
+            fn = getattr(lib, name)
+            fn.restype = ctypes.c_int
+            fn.argtypes = [p, p, sz, p, p, p, p, sz, ctypes.c_uint32, ctypes.c_int32, p]
+        lib.gsdrxIirSinglePassStatus.restype = ctypes.c_int
+        lib.gsdrxIirSinglePassStatus.argtypes = [ctypes.c_int32, p]
+        _probes.append(lib)
+    return _probes[0]
+
+
+def single_pass(bd, ad, xd, xh=None, yh=None, max_polls=1 << 22):
+    """gsdrxIirFFSinglePass / CC of the probes build on torch tensors (ops.iir's contract); returns (rc, y)."""
+    lib = probes_lib()
+    y = torch.empty_like(xd)
+    fn = lib.gsdrxIirCCSinglePass if xd.dtype == torch.complex64 else lib.gsdrxIirFFSinglePass
+    ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+    rc = fn(bd.data_ptr(), ad.data_ptr(), bd.numel(), ptr(xh), ptr(yh), xd.data_ptr(), y.data_ptr(), xd.numel(),
+            max_polls, xd.device.index, torch.cuda.current_stream(xd.device).cuda_stream)
+    return rc, y
+
+
+@pytest.fixture(params=["scan", "single_pass"])
+def iir_fn(request, cuda):
+    """Every parity test runs on both IIR formulations: the multi-pass scan (gsdrIirFF / gsdrIirCC, the product) and
+    the single-pass kernel (probes build, chosen per call; K <= 9 only -- it refuses larger K with
+    hipErrorNotSupported, which those cases check). After each single-pass call the device status word must be
+    clear (no tile gave up waiting)."""
+    from gsdr_amd import ops
+
+    if request.param == "scan":
+        return ops.iir
+
+    def run(bd, ad, xd, xh=None, yh=None):
+        rc, y = single_pass(bd, ad, xd, xh, yh)
+        if bd.numel() > 9:
+            assert rc == HIP_ERROR_NOT_SUPPORTED
+            pytest.skip("single-pass kernel: K <= 9")
+        assert rc == 0
+        assert probes_lib().gsdrxIirSinglePassStatus(cuda.index, torch.cuda.current_stream(cuda).cuda_stream) == 0
+        return y
+
+    return run
 
 
 def bar(b, a, x, want, xh=None, yh=None):
@@ -57,15 +106,13 @@ SIZES = [1, 2, 5, 127, 128, 129, 1000, 8192, 8193, 128 * 64 + 1, 128 * 64 * 64 +
 
 @pytest.mark.parametrize("n", SIZES)
 @pytest.mark.parametrize("cplx", [False, True])
-def test_iir_butter4_sizes(cuda, n, cplx):
-    from gsdr_amd import ops
-
+def test_iir_butter4_sizes(cuda, iir_fn, n, cplx):
     b, a = design("butter", 4)
     rng = np.random.default_rng(n)
     x = rng.uniform(-1, 1, n).astype(np.float32)
     if cplx:
         x = (x + 1j * rng.uniform(-1, 1, n)).astype(np.complex64)
-    y = ops.iir(dev(b, cuda), dev(a, cuda), dev(x, cuda)).cpu().numpy()
+    y = iir_fn(dev(b, cuda), dev(a, cuda), dev(x, cuda)).cpu().numpy()
     want, _, _ = o.iir(b, a, x)
     e = err(y, want)
     print(f"n={n} cplx={cplx} err={e:.2e}")
@@ -74,9 +121,7 @@ def test_iir_butter4_sizes(cuda, n, cplx):
 
 @pytest.mark.parametrize("kind,order", [("butter", 1), ("butter", 2), ("butter", 3), ("butter", 6), ("poles", 5),
                                         ("poles", 9), ("poles", 16), ("poles", 20), ("poles", 31)])
-def test_iir_orders_with_history(cuda, kind, order):
-    from gsdr_amd import ops
-
+def test_iir_orders_with_history(cuda, iir_fn, kind, order):
     b, a = design(kind, order)
     rng = np.random.default_rng(order)
     n = 200_003
@@ -84,7 +129,7 @@ def test_iir_orders_with_history(cuda, kind, order):
     xh = rng.uniform(-1, 1, order).astype(np.float32)
     yh = rng.uniform(-1, 1, order).astype(np.float32)
     xh_d, yh_d = dev(xh, cuda), dev(yh, cuda)
-    y = ops.iir(dev(b, cuda), dev(a, cuda), dev(x, cuda), xh_d, yh_d).cpu().numpy()
+    y = iir_fn(dev(b, cuda), dev(a, cuda), dev(x, cuda), xh_d, yh_d).cpu().numpy()
     want, xh2, yh2 = o.iir(b, a, x, xh, yh)
     e = err(y, want)
     print(f"{kind}{order} err={e:.2e} seq32={err(o.iir_f32(b, a, x, xh, yh), want):.2e}")
@@ -95,15 +140,13 @@ def test_iir_orders_with_history(cuda, kind, order):
 
 @pytest.mark.parametrize("order", [4, 6])
 @pytest.mark.parametrize("cplx", [False, True])
-def test_iir_chunked_calls_continue(cuda, order, cplx):
+def test_iir_chunked_calls_continue(cuda, iir_fn, order, cplx):
     """Consecutive calls continue one recursion through the history buffers. Every call is checked
     against the float64 oracle started from the history the GPU handed over (the property that holds
     for any filter); for the well-conditioned 4th-order filter the concatenation is also checked
     against one monolithic evaluation. (Direct-form 6th order at 0.1 fs amplifies a state difference
     ~200-1000x: float32 history values that are each within rounding of the true state can move the
     next call's outputs by ~1e-2, as they would for any float32 implementation fed those values.)"""
-    from gsdr_amd import ops
-
     b, a = design("butter", order)
     rng = np.random.default_rng(7)
     n = 100_000
@@ -122,7 +165,7 @@ def test_iir_chunked_calls_continue(cuda, order, cplx):
         if m == 0:
             break
         hx, hy = xh.cpu().numpy().copy(), yh.cpu().numpy().copy()
-        y = ops.iir(bd, ad, xd[pos:pos + m], xh, yh).cpu().numpy()
+        y = iir_fn(bd, ad, xd[pos:pos + m], xh, yh).cpu().numpy()
         w, _, _ = o.iir(b, a, x[pos:pos + m], hx, hy)
         assert err(y, w) <= IIR_TOL, (pos, m)
         parts.append(y)
@@ -157,19 +200,17 @@ def test_iir_impulse_and_validation(cuda):
 
 @pytest.mark.parametrize("order,n", [(4, 1 << 25), (4, (1 << 25) + 1), (8, (1 << 21) + 3), (2, (1 << 22) + 9),
                                      (1, 3 * (1 << 21) + 1), (6, 64 * 64 * 32 * 3 + 5)])
-def test_iir_scan_paths(cuda, order, n):
+def test_iir_scan_paths(cuda, iir_fn, order, n):
     """Levels >= 2 and level 1's down-sweep run in one launch (k_iir_scan_upper) up to 256 level-2
     elements (2^25 samples); past that, the per-level launches. Inputs at and past the limit, partial
     groups at every level, and a level-2 scan of one group (levels == 2), each against the float64
     oracle with history."""
-    from gsdr_amd import ops
-
     b, a = design("poles", order)
     rng = np.random.default_rng(n)
     x = rng.uniform(-1, 1, n).astype(np.float32)
     xh = rng.uniform(-1, 1, order).astype(np.float32)
     yh = rng.uniform(-1, 1, order).astype(np.float32)
-    y = ops.iir(dev(b, cuda), dev(a, cuda), dev(x, cuda), dev(xh, cuda), dev(yh, cuda)).cpu().numpy()
+    y = iir_fn(dev(b, cuda), dev(a, cuda), dev(x, cuda), dev(xh, cuda), dev(yh, cuda)).cpu().numpy()
     want, _, _ = o.iir(b, a, x, xh, yh)
     e = err(y, want)
     print(f"order={order} n={n} err={e:.2e}")
@@ -179,13 +220,11 @@ def test_iir_scan_paths(cuda, order, n):
 @pytest.mark.parametrize("order", [1, 2])
 @pytest.mark.parametrize("n", [3 * 8192 + 1, 3 * (1 << 21) + 5])
 @pytest.mark.parametrize("cplx", [False, True])
-def test_iir_slow_decay_carries(cuda, order, n, cplx):
+def test_iir_slow_decay_carries(cuda, iir_fn, order, n, cplx):
     """Poles at radius 1 - 1e-6: the state entering a tile carries weight ~e^-2 across a superblock of 2^21
     samples, so a carry dropped or misordered anywhere in the single-pass scan (chunks within a wave,
     waves within a tile, tiles within a superblock, superblocks) shows at O(1) rather than under the
     tolerance, as it would for a fast-decaying filter. DC input plus noise keeps the output O(1)."""
-    from gsdr_amd import ops
-
     r = 1.0 - 1e-6
     a = np.poly([r] if order == 1 else [r * np.exp(3e-3j), r * np.exp(-3e-3j)]).real.astype(np.float32)
     b = np.zeros(order + 1, np.float32)
@@ -194,8 +233,40 @@ def test_iir_slow_decay_carries(cuda, order, n, cplx):
     x = rng.uniform(0, 1, n).astype(np.float32)
     if cplx:
         x = (x + 1j * rng.uniform(-1, 0, n)).astype(np.complex64)
-    y = ops.iir(dev(b, cuda), dev(a, cuda), dev(x, cuda)).cpu().numpy()
+    y = iir_fn(dev(b, cuda), dev(a, cuda), dev(x, cuda)).cpu().numpy()
     want, _, _ = o.iir(b, a, x)
     e = float(np.max(np.abs(y - want))) / float(np.max(np.abs(want)))
     print(f"order={order} n={n} cplx={cplx} err={e:.2e} peak={float(np.max(np.abs(want))):.3g}")
     assert e <= 1e-5
+
+
+def test_iir_single_pass_give_up_is_reported(cuda):
+    """The single-pass kernel's bounded waits: with maxPolls = 0 every tile that has to wait for an earlier tile
+    gives up at once. The call itself returns hipSuccess (the kernel cannot fail a launch), but
+    gsdrxIirSinglePassStatus then reports hipErrorLaunchFailure (and clears the word), the outputs past the
+    first tile are NaN rather than plausible values, and the caller's history buffers are left as they were (the
+    last tile did not wait for the readers). The first tile, which waits for nothing, is still exact."""
+    lib = probes_lib()
+    st = torch.cuda.current_stream(cuda).cuda_stream
+    assert lib.gsdrxIirSinglePassStatus(cuda.index, st) == 0
+    b, a = design("butter", 4)
+    bd, ad = dev(b, cuda), dev(a, cuda)
+    n = 5 * 8192 + 17  # six tiles of 8192 real samples
+    x = np.random.default_rng(11).uniform(-1, 1, n).astype(np.float32)
+    xh0 = np.full(4, 0.25, np.float32)
+    yh0 = np.full(4, -0.5, np.float32)
+    xh, yh = dev(xh0.copy(), cuda), dev(yh0.copy(), cuda)
+    rc, y = single_pass(bd, ad, dev(x, cuda), xh, yh, max_polls=0)
+    assert rc == 0
+    assert lib.gsdrxIirSinglePassStatus(cuda.index, st) == HIP_ERROR_LAUNCH_FAILURE
+    assert lib.gsdrxIirSinglePassStatus(cuda.index, st) == 0  # cleared by the query
+    yc = y.cpu().numpy()
+    want, _, _ = o.iir(b, a, x, xh0, yh0)
+    assert err(yc[:8192], want[:8192]) <= IIR_TOL
+    assert np.isnan(yc[8192:]).all()
+    assert np.array_equal(xh.cpu().numpy(), xh0) and np.array_equal(yh.cpu().numpy(), yh0)
+    # the normal bound on the same call: exact, status clear, history advanced
+    rc, y = single_pass(bd, ad, dev(x, cuda), xh, yh)
+    assert rc == 0 and lib.gsdrxIirSinglePassStatus(cuda.index, st) == 0
+    assert err(y.cpu().numpy(), want) <= IIR_TOL
+    assert not np.array_equal(xh.cpu().numpy(), xh0)

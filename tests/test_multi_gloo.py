@@ -141,3 +141,59 @@ def test_aggregate_is_weak_scaling():
     eight = bench.aggregate(bench.N_IN, 8, 10, 1.0e-3)
     assert eight == pytest.approx(8 * one)
     assert one == pytest.approx(bench.N_IN * 10 / 1.0e-3 / 1e6)
+
+
+def test_launch_cmd_and_env():
+    """bench.launch_cmd / launch_env: the torchrun child a plain `python bench.py --gpus N` starts."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    cmd = bench.launch_cmd(8, 29512, ["--gpus", "8", "--steps", "20", "--warmup", "5"])
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in cmd and "--nnodes=1" in cmd and "--master-port=29512" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-7:] == [os.path.join(ROOT, "bench.py"), "--gpus", "8", "--steps", "20", "--warmup", "5"]
+    os.environ["RANK"] = "3"  # stale rank variables of an outer job must not leak into the child
+    try:
+        env = bench.launch_env(29512)
+    finally:
+        del os.environ["RANK"]
+    assert env["MASTER_ADDR"] == "127.0.0.1" and env["MASTER_PORT"] == "29512" and "RANK" not in env
+
+
+@pytest.mark.timeout(240)
+def test_plain_bench_self_launches_ranks():
+    """`python bench.py --gpus 2` outside torchrun starts its own two rank processes: each rank sees RANK /
+    LOCAL_RANK / WORLD_SIZE and the 127.0.0.1 rendezvous the parent chose (BENCH_LAUNCH_PROBE: the ranks
+    report their environment and stop before any device work, so this runs on the CPU)."""
+    import json
+    import subprocess
+
+    env = dict(os.environ, BENCH_REHEARSE="1", BENCH_LAUNCH_PROBE="1", BENCH_LAUNCH_PRINT="1")
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3"], cwd=ROOT,
+                       env=env, capture_output=True, text=True, timeout=200)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    lines = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+    launch = [d for d in lines if "cmd" in d]
+    ranks = sorted((d for d in lines if "rank" in d), key=lambda d: d["rank"])
+    assert len(launch) == 1 and "--nproc-per-node=2" in launch[0]["cmd"]
+    port = str(launch[0]["port"])
+    assert [(d["rank"], d["local_rank"], d["world"]) for d in ranks] == [(0, 0, 2), (1, 1, 2)]
+    assert all(d["master"] == ["127.0.0.1", port] for d in ranks)
+
+
+@pytest.mark.timeout(120)
+def test_plain_bench_refuses_without_enough_gpus():
+    """Without BENCH_REHEARSE, `python bench.py --gpus 2` on a box with fewer than two visible GPUs (here: none)
+    refuses before starting any rank, with a message and no JSON line."""
+    import subprocess
+
+    env = dict(os.environ)
+    for k in ("BENCH_REHEARSE", "RANK", "LOCAL_RANK", "WORLD_SIZE"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=100)
+    assert r.returncode == 2 and "needs 2 visible GPUs" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

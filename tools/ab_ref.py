@@ -2,7 +2,8 @@
 """Side-by-side timing of the working tree's libgsdr.so against an earlier build (development tool):
     python tools/ab_ref.py build/ref_50fdf7b/libgsdr.so
 Each entry point on its bench shape, both libraries interleaved over ROUNDS rounds in one process on the same
-buffers (HIP events around back-to-back launches; min over rounds), so box-to-box spread cancels."""
+buffers (HIP events around back-to-back launches; min over rounds), so box-to-box spread cancels. Inputs and outputs
+rotate over 3 buffer sets, as bench.py's do, so no launch re-reads or re-writes a buffer the Infinity Cache holds."""
 import ctypes
 import os
 import sys
@@ -20,6 +21,7 @@ SIGS = {
     "gsdrFirFC": [sz, p, sz, p, p, sz, i32, p],
     "gsdrFirFF": [sz, p, sz, p, p, sz, i32, p],
     "gsdrFmDemod": [f, f, f, f, u32, sz, p, sz, p, p, sz, i32, p],
+    "gsdrAmDemod": [f, f, f, u32, sz, p, sz, p, p, sz, i32, p],
     "gsdrxFmDemodInt8": [f, f, f, f, u32, sz, p, sz, p, p, sz, i32, p],
     "gsdrxAmDemodInt8": [f, f, f, u32, sz, p, sz, p, p, sz, i32, p],
     "gsdrxFirFCInt8": [sz, p, sz, p, p, sz, i32, p],
@@ -48,53 +50,56 @@ def main():
     D, T, NO = 4, 127, 1 << 24
     NI = (NO - 1) * D + T
     taps = torch.from_numpy(lowpass_taps(T, 0.1)).to(dev)
-    xs = [(torch.rand(2 * NI, device=dev, generator=g) * 2 - 1).view(torch.complex64) for _ in range(2)]
-    x8s = [torch.randint(-100, 100, (2 * NI,), dtype=torch.int8, device=dev, generator=g) for _ in range(2)]
-    yc = torch.empty(NO, dtype=torch.complex64, device=dev)
-    yf = torch.empty(NO, dtype=torch.float32, device=dev)
+    K = 3
+    xs = [(torch.rand(2 * NI, device=dev, generator=g) * 2 - 1).view(torch.complex64) for _ in range(K)]
+    x8s = [torch.randint(-100, 100, (2 * NI,), dtype=torch.int8, device=dev, generator=g) for _ in range(K)]
+    ycs = [torch.empty(NO, dtype=torch.complex64, device=dev) for _ in range(K)]
+    yfs = [torch.empty(NO, dtype=torch.float32, device=dev) for _ in range(K)]
     n5 = 1 << 24
     t1 = torch.rand(63, device=dev, generator=g)  # config 1: 2^20 real outputs, 63 taps, D = 1
     x1 = torch.rand((1 << 20) + 62, device=dev, generator=g)
     y1 = torch.empty(1 << 20, device=dev)
-    syms = torch.randint(0, 256, (n5,), dtype=torch.uint8, device=dev, generator=g)
-    rx = torch.empty(n5, dtype=torch.complex64, device=dev)
-    dec = torch.empty(n5, dtype=torch.uint8, device=dev)
+    symss = [torch.randint(0, 256, (n5,), dtype=torch.uint8, device=dev, generator=g) for _ in range(K)]
+    rxs = [torch.empty(n5, dtype=torch.complex64, device=dev) for _ in range(K)]
+    decs = [torch.empty(n5, dtype=torch.uint8, device=dev) for _ in range(K)]
     from scipy import signal as sps
 
     bb, aa = (torch.tensor(v, dtype=torch.float32, device=dev) for v in sps.butter(4, 0.1))
     bb8, aa8 = (torch.tensor(v, dtype=torch.float32, device=dev) for v in sps.butter(8, 0.2))
-    xi = torch.rand(n5, device=dev, generator=g)
-    yi = torch.empty_like(xi)
-    xic = torch.rand(2 * n5, device=dev, generator=g).view(torch.complex64)
-    yic = torch.empty_like(xic)
+    xis = [torch.rand(n5, device=dev, generator=g) for _ in range(4)]
+    yis = [torch.empty_like(x) for x in xis]
+    xics = [torch.rand(2 * n5, device=dev, generator=g).view(torch.complex64) for _ in range(4)]
+    yics = [torch.empty_like(x) for x in xics]
     for lib in L:
         assert lib.gsdrQpsk256InitConstellation(0, 1.0, 0, st) == 0
     cases = {
         "gsdrFirFF1": lambda lib, k: lib.gsdrFirFF(1, t1.data_ptr(), 63, x1.data_ptr(), y1.data_ptr(), 1 << 20, 0, st),
-        "gsdrFirFC": lambda lib, k: lib.gsdrFirFC(D, taps.data_ptr(), T, xs[k % 2].data_ptr(), yc.data_ptr(), NO, 0, st),
-        "gsdrFmDemod": lambda lib, k: lib.gsdrFmDemod(1e6, 0.0, 1e5, 2e4, D, 0, taps.data_ptr(), T, xs[k % 2].data_ptr(),
-                                                      yf.data_ptr(), NO - 1, 0, st),
-        "gsdrxFirFCInt8": lambda lib, k: lib.gsdrxFirFCInt8(D, taps.data_ptr(), T, x8s[k % 2].data_ptr(), yc.data_ptr(),
+        "gsdrFirFC": lambda lib, k: lib.gsdrFirFC(D, taps.data_ptr(), T, xs[k % K].data_ptr(), ycs[k % K].data_ptr(), NO, 0, st),
+        "gsdrFmDemod": lambda lib, k: lib.gsdrFmDemod(1e6, 0.0, 1e5, 2e4, D, 0, taps.data_ptr(), T, xs[k % K].data_ptr(),
+                                                      yfs[k % K].data_ptr(), NO - 1, 0, st),
+        "gsdrAmDemod": lambda lib, k: lib.gsdrAmDemod(1e6, 0.0, 1e5, D, 0, taps.data_ptr(), T, xs[k % K].data_ptr(),
+                                                      yfs[k % K].data_ptr(), NO, 0, st),
+        "gsdrxFirFCInt8": lambda lib, k: lib.gsdrxFirFCInt8(D, taps.data_ptr(), T, x8s[k % K].data_ptr(), ycs[k % K].data_ptr(),
                                                             NO, 0, st),
         "gsdrxFmDemodInt8": lambda lib, k: lib.gsdrxFmDemodInt8(1e6, 0.0, 1e5, 2e4, D, 0, taps.data_ptr(), T,
-                                                                x8s[k % 2].data_ptr(), yf.data_ptr(), NO - 1, 0, st),
+                                                                x8s[k % K].data_ptr(), yfs[k % K].data_ptr(), NO - 1, 0, st),
         "gsdrxAmDemodInt8": lambda lib, k: lib.gsdrxAmDemodInt8(1e6, 0.0, 1e5, D, 0, taps.data_ptr(), T,
-                                                                x8s[k % 2].data_ptr(), yf.data_ptr(), NO - 1, 0, st),
-        "gsdrxQpsk256ModulateAwgn": lambda lib, k: lib.gsdrxQpsk256ModulateAwgn(syms.data_ptr(), rx.data_ptr(), n5, 0,
+                                                                x8s[k % K].data_ptr(), yfs[k % K].data_ptr(), NO - 1, 0, st),
+        "gsdrxQpsk256ModulateAwgn": lambda lib, k: lib.gsdrxQpsk256ModulateAwgn(symss[k % K].data_ptr(), rxs[k % K].data_ptr(), n5, 0,
                                                                                 0.02, 0x5EED0005, 0, 0, st),
-        "gsdrQpsk256Demodulate": lambda lib, k: lib.gsdrQpsk256Demodulate(rx.data_ptr(), dec.data_ptr(), n5, 0, 0, st),
+        "gsdrQpsk256Demodulate": lambda lib, k: lib.gsdrQpsk256Demodulate(rxs[k % K].data_ptr(), decs[k % K].data_ptr(), n5, 0, 0, st),
         # config 5's round trip: modulate + AWGN, then demodulate what it wrote
-        "config5_round_trip": lambda lib, k: (lib.gsdrxQpsk256ModulateAwgn(syms.data_ptr(), rx.data_ptr(), n5, 0, 0.02,
+        "config5_round_trip": lambda lib, k: (lib.gsdrxQpsk256ModulateAwgn(symss[k % K].data_ptr(), rxs[k % K].data_ptr(), n5, 0, 0.02,
                                                                            0x5EED0005, 0, 0, st),
-                                              lib.gsdrQpsk256Demodulate(rx.data_ptr(), dec.data_ptr(), n5, 0, 0, st))[1],
-        "gsdrIirFF": lambda lib, k: lib.gsdrIirFF(bb.data_ptr(), aa.data_ptr(), 5, None, None, xi.data_ptr(),
-                                                  yi.data_ptr(), n5, 0, st),
-        "gsdrIirCC": lambda lib, k: lib.gsdrIirCC(bb.data_ptr(), aa.data_ptr(), 5, None, None, xic.data_ptr(),
-                                                  yic.data_ptr(), n5, 0, st),
-        "gsdrIirFF9": lambda lib, k: lib.gsdrIirFF(bb8.data_ptr(), aa8.data_ptr(), 9, None, None, xi.data_ptr(),
-                                                   yi.data_ptr(), n5, 0, st),
-        "gsdrIirCC9": lambda lib, k: lib.gsdrIirCC(bb8.data_ptr(), aa8.data_ptr(), 9, None, None, xic.data_ptr(),
-                                                   yic.data_ptr(), n5, 0, st),
+                                              lib.gsdrQpsk256Demodulate(rxs[k % K].data_ptr(), decs[k % K].data_ptr(), n5, 0, 0, st))[1],
+        "gsdrIirFF": lambda lib, k: lib.gsdrIirFF(bb.data_ptr(), aa.data_ptr(), 5, None, None, xis[k % 4].data_ptr(),
+                                                  yis[k % 4].data_ptr(), n5, 0, st),
+        "gsdrIirCC": lambda lib, k: lib.gsdrIirCC(bb.data_ptr(), aa.data_ptr(), 5, None, None, xics[k % 4].data_ptr(),
+                                                  yics[k % 4].data_ptr(), n5, 0, st),
+        "gsdrIirFF9": lambda lib, k: lib.gsdrIirFF(bb8.data_ptr(), aa8.data_ptr(), 9, None, None, xis[k % 4].data_ptr(),
+                                                   yis[k % 4].data_ptr(), n5, 0, st),
+        "gsdrIirCC9": lambda lib, k: lib.gsdrIirCC(bb8.data_ptr(), aa8.data_ptr(), 9, None, None, xics[k % 4].data_ptr(),
+                                                   yics[k % 4].data_ptr(), n5, 0, st),
     }
     only = os.environ.get("CASES")
     res = {}

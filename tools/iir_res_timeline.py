@@ -1,11 +1,10 @@
 """Per-tile phase timeline of the single-pass IIR kernel (development tool). Needs the timing build:
-    tools/variant_lib.sh timing gsdr_amd/csrc/iir.hip -DGSDR_IIR_RES_TIMING
+    tools/variant_lib.sh timing gsdr_amd/csrc/iir.hip -DGSDR_TUNING_PROBES -DGSDR_IIR_RES_TIMING
 which writes each tile's wall-clock marks (100 MHz) over the first words of its output instead of y.
 Prints per-phase medians for 2^24 samples (4th / 8th-order Butterworth, real and complex)."""
 import ctypes, os, sys, numpy as np, torch
 from scipy import signal as sps
 lib = ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "build", "var_timing", "libgsdr.so"))
-lib.gsdrxIirSetSinglePass(1)
 dev = torch.device("cuda:0")
 n = 1 << 24
 P = ctypes.c_void_p
@@ -15,9 +14,10 @@ for name, K, order, cplx in (("FF5", 5, 4, False), ("CC5", 5, 4, True), ("FF9", 
     x = torch.rand(2 * n if cplx else n, device=dev)
     y = torch.empty_like(x)
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    fn = lib.gsdrIirCC if cplx else lib.gsdrIirFF
+    fn = lib.gsdrxIirCCSinglePass if cplx else lib.gsdrxIirFFSinglePass
     for _ in range(5):
-        fn(P(bb.data_ptr()), P(aa.data_ptr()), ctypes.c_size_t(K), None, None, P(x.data_ptr()), P(y.data_ptr()), ctypes.c_size_t(n), 0, st)
+        fn(P(bb.data_ptr()), P(aa.data_ptr()), ctypes.c_size_t(K), None, None, P(x.data_ptr()), P(y.data_ptr()), ctypes.c_size_t(n),
+           ctypes.c_uint32(1 << 22), 0, st)
     torch.cuda.synchronize()
     TS = 4096 if cplx else 8192   # samples a tile
     per = TS * (2 if cplx else 1)  # floats a tile

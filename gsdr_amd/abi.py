@@ -76,6 +76,7 @@ SIGNATURES = {
     # qpsk256.h
     "gsdrQpsk256Modulate": (_err, [_p, _p, _u32, _f, _u32, _i32, _p]),
     "gsdrxQpsk256ModulateAwgn": (_err, [_p, _p, _u32, _u32, _f, _u64, _u64, _i32, _p]),
+    "gsdrxQpsk256ModulateAwgnDemodulate": (_err, [_p, _p, _p, _u32, _u32, _f, _u64, _u64, _i32, _p]),
     "gsdrQpsk256Demodulate": (_err, [_p, _p, _u32, _u32, _i32, _p]),
     "gsdrQpsk256Modulate4x": (_err, [_p, _p, _p, _p, _p, _p, _p, _p, _u32, _f, _u32, _i32, _p]),
     "gsdrQpsk256Demodulate4x": (_err, [_p, _p, _p, _p, _p, _p, _p, _p, _u32, _u32, _i32, _p]),

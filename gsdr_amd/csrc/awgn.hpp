@@ -34,7 +34,7 @@ namespace gsdr {
 
 constexpr int kAwgnTableSize = 21 * 32;
 
-// (R, S) pairs; copied into LDS by the kernel that uses them (awgn_load_table).
+// (R, S) pairs; copied into LDS by the kernel that uses them (awgn_fetch_table, awgn_store_table).
 __constant__ float2 c_awgn_table[kAwgnTableSize] = {
 #define GSDR_AWGN_ENTRY(r, s) {r, s},
 #include "awgn_table.inc"
@@ -93,26 +93,45 @@ __device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t
 #if defined(GSDR_AWGN_PAIRS) && !defined(GSDR_TUNING_PROBES)
 #error "GSDR_AWGN_PAIRS is a timing probe: probe builds only"
 #endif
+constexpr int kAwgnLdsSize = 3 * 256;  // the table padded to three entries a thread (awgn_store_table)
 struct AwgnLds {
 #ifdef GSDR_AWGN_PAIRS
-  float2 rs[kAwgnTableSize];
+  float2 rs[kAwgnLdsSize];
 #else
-  float r[kAwgnTableSize], s[kAwgnTableSize];
+  float r[kAwgnLdsSize], s[kAwgnLdsSize];
 #endif
 };
 // Entries below kAwgnTailIndex serve only tail components (a < 32 <=> x = 2 a + 1 < 64 <=> index < 6 * 32),
 // whose values the tail extension replaces: their R is NaN in LDS, so a tail component turns its symbol's
 // noisy output into NaN and one NaN test over a lane's outputs finds it (awgn_has_tail).
 constexpr uint32_t kAwgnTailIndex = 6 * 32;
-__device__ __forceinline__ void awgn_load_table(AwgnLds& t, uint32_t nthreads) {
-  for (uint32_t i = threadIdx.x; i < (uint32_t)kAwgnTableSize; i += nthreads) {
-    float2 e = c_awgn_table[i];
+// The table's copy into LDS in two halves, so the caller can issue other loads between them: awgn_fetch_table
+// loads a 256-thread workgroup's entries (thread t: t, t + 256, t + 512) into registers, awgn_store_table writes
+// them (entries below kAwgnTailIndex with R = NaN). The caller's barrier publishes the table.
+struct AwgnRegs {
+  float2 e[3];
+};
+__device__ __forceinline__ AwgnRegs awgn_fetch_table() {
+  static_assert(kAwgnTableSize <= 3 * 256 && kAwgnTableSize > 2 * 256, "three entries a thread of 256");
+  AwgnRegs r;
+  const uint32_t t = threadIdx.x;
+  r.e[0] = c_awgn_table[t];
+  r.e[1] = c_awgn_table[t + 256];
+  r.e[2] = c_awgn_table[t + 512 < (uint32_t)kAwgnTableSize ? t + 512 : t];
+  return r;
+}
+__device__ __forceinline__ void awgn_store_table(AwgnLds& tab, const AwgnRegs& r) {
+  static_assert(kAwgnLdsSize == 3 * 256, "three entries a thread");
+#pragma unroll
+  for (uint32_t k = 0; k < 3; ++k) {  // (entries past the table land in the padding: no branch around the loads)
+    const uint32_t i = threadIdx.x + 256u * k;
+    float2 e = r.e[k];
     if (i < kAwgnTailIndex) e.x = __builtin_nanf("");
 #ifdef GSDR_AWGN_PAIRS
-    t.rs[i] = e;
+    tab.rs[i] = e;
 #else
-    t.r[i] = e.x;
-    t.s[i] = e.y;
+    tab.r[i] = e.x;
+    tab.s[i] = e.y;
 #endif
   }
 }

@@ -38,8 +38,8 @@ struct FirJob {
   uint32_t nco_n0 = 0;
   float fm_gain = 0.0f;
   uint32_t out_phase = 0;  // absolute index of output 0 mod 16 (fir_i8_mfma.hpp)
-  uint32_t q0 = 0;         // chains: absolute index of output 0 (firstSampleIndex / D), low 32 bits -- the
-                           // anchored polyphase tiles' NCO cell grid (fir_engine.hpp, stage_tile_rel)
+  uint64_t q0 = 0;         // chains: absolute index of output 0 (firstSampleIndex / D) -- the anchored
+                           // polyphase tiles' NCO cell grid (fir_engine.hpp, stage_tile_rel)
   // the int8 matrix-core kernels' streaming inputs (FirParams)
   int64_t in_off = 0;
   const void* hist = nullptr;
@@ -129,28 +129,29 @@ hipError_t launch_generic(const FirJob& j, hipStream_t s) {
 }
 
 // Tile grid of the polyphase kernels. FIR: tile t = outputs [t KT, (t + 1) KT). FM / AM chains (anchored NCO,
-// fir_engine.hpp stage_tile_rel): tiles on the absolute output grid -- output 0 (absolute index q0) sits at
-// tile_shift = q0 mod KT in tile 0, which is sub-tile cell_sub0 of its NCO cell of SUBS tiles (CELL = SUBS KT
-// outputs; the short-call shapes of a decimation are sub-tiles of its largest tile). Returns the tile count.
+// fir_engine.hpp stage_tile_rel): tiles on an absolute output grid of stride S -- KT for AM; KT - R for FM, whose
+// tiles overlap by one thread's outputs so that every discriminator pairs two outputs of one tile -- output 0
+// (absolute index q0) sits at tile_shift = q0 mod S in tile 0, which is sub-tile cell_sub0 of its NCO cell of
+// SUBS tiles (CELL = SUBS S outputs; the short-call shapes of a decimation are sub-tiles of its largest tile, whose
+// stride is SUBS times theirs). Returns the tile count.
 template <int MODE>
-inline uint64_t poly_grid(const FirJob& j, FirParams& p, uint32_t kt, uint32_t subs) {
-  p.tile_stride = kt;
+inline uint64_t poly_grid(const FirJob& j, FirParams& p, uint32_t kt, uint32_t r, uint32_t subs) {
+  const uint32_t stride = MODE == kModeFm ? kt - r : kt;
+  p.tile_stride = stride;
   if constexpr (MODE == kModeFir) {
     p.tile_shift = 0;
     p.cell_sub0 = 0;
   } else {
-    p.tile_shift = j.q0 % kt;
-    p.cell_sub0 = (j.q0 / kt) % subs;
+    p.tile_shift = (uint32_t)(j.q0 % stride);
+    p.cell_sub0 = (uint32_t)((j.q0 % ((uint64_t)stride * subs)) / stride);
   }
-  return ceil_div<uint64_t>(j.N + p.tile_shift, kt);
+  return ceil_div<uint64_t>(j.N + p.tile_shift, stride);
 }
 
 template <class TapT, class InT, int D, int R, int JC, int WG, int MODE, int ABL = 0, bool NT = false, bool XM = false,
-          int CST = 0, bool DMA = false, int SUBS = 1, int FMB = 0>
+          int CST = 0, bool DMA = false, int SUBS = 1>
 hipError_t launch_poly(const FirJob& j, hipStream_t s) {
   using Geo = TileGeo<InT, D, R, WG>;
-  static_assert(Geo::KT / (FMB > 0 ? FMB : Geo::KT) <= 4, "at most 4 FM partner blocks a tile (poly_lds_bytes)");
-  static_assert(((Geo::KT * SUBS) & (Geo::KT * SUBS - 1)) == 0, "NCO cells must be a power of two outputs");
   FirParams p = make_params(j);
   const uint64_t rows = ceil_div<uint64_t>(j.T, (uint64_t)D);
   const uint64_t nch = ceil_div<uint64_t>(rows, (uint64_t)JC);
@@ -159,22 +160,22 @@ hipError_t launch_poly(const FirJob& j, hipStream_t s) {
   const size_t lds = poly_lds_bytes<InT, D, R, WG>((uint32_t)span, MODE);
   if (lds > kMaxTileLds) return launch_generic<TapT, InT, MODE>(j, s);
   p.nch = (uint32_t)nch;
-  const uint32_t stride = Geo::KT;
-  const uint64_t tiles = poly_grid<MODE>(j, p, Geo::KT, SUBS);
+  const uint64_t tiles = poly_grid<MODE>(j, p, Geo::KT, R, SUBS);
+  const uint32_t stride = p.tile_stride;
   if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
   constexpr uint64_t A = SampleT<InT>::kSrcAlign;
   // (the anchored grid moves every tile start by tile_shift * D samples: a whole number of aligned units, D even)
   const bool vec = (reinterpret_cast<uintptr_t>(j.in) % A) == 0 && ((uint64_t)stride * D * sizeof(InT)) % A == 0;
   if (vec) {
-    k_fir_poly<TapT, InT, D, R, JC, WG, true, MODE, ABL, NT, XM, CST, DMA, 0, SUBS, FMB>
+    k_fir_poly<TapT, InT, D, R, JC, WG, true, MODE, ABL, NT, XM, CST, DMA, 0, SUBS>
         <<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
   } else if (shifted_staging<InT>(j.in, (uint64_t)stride * D)) {
     launch_shifted<InT>(j.in, [&](auto sh) {
-      k_fir_poly<TapT, InT, D, R, JC, WG, false, MODE, ABL, NT, XM, CST, false, decltype(sh)::value, SUBS, FMB>
+      k_fir_poly<TapT, InT, D, R, JC, WG, false, MODE, ABL, NT, XM, CST, false, decltype(sh)::value, SUBS>
           <<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
     });
   } else {
-    k_fir_poly<TapT, InT, D, R, JC, WG, false, MODE, ABL, NT, XM, CST, DMA, 0, SUBS, FMB>
+    k_fir_poly<TapT, InT, D, R, JC, WG, false, MODE, ABL, NT, XM, CST, DMA, 0, SUBS>
         <<<dim3((uint32_t)tiles), dim3(WG), lds, s>>>(p);
   }
   return launch_status();
@@ -289,7 +290,7 @@ hipError_t launch_d4_complex(const FirJob& j, hipStream_t s) {
 // choice as launch_poly, so each channel is that kernel's call bit for bit). Returns
 // hipErrorNotSupported, before launching anything, when the shape does not apply (the caller then runs
 // the channels one by one).
-template <class TapT, class InT, int D, int R, int JC, int WG, int MODE, int FMB = 0>
+template <class TapT, class InT, int D, int R, int JC, int WG, int MODE>
 hipError_t launch_multi_grouped(const FirJob& j, const MultiParams& mp, hipStream_t s) {
   using Geo = TileGeo<InT, D, R, WG>;
   FirParams p = make_params(j);
@@ -300,20 +301,20 @@ hipError_t launch_multi_grouped(const FirJob& j, const MultiParams& mp, hipStrea
   const size_t lds = poly_lds_bytes<InT, D, R, WG>((uint32_t)span, MODE);
   if (lds > kMaxTileLds) return hipErrorNotSupported;
   p.nch = (uint32_t)nch;
-  const uint32_t stride = Geo::KT;
-  const uint64_t tiles = poly_grid<MODE>(j, p, Geo::KT, 1);
+  const uint64_t tiles = poly_grid<MODE>(j, p, Geo::KT, R, 1);
+  const uint32_t stride = p.tile_stride;
   const uint64_t blocks = ceil_div<uint64_t>(tiles, 8) * 8 * mp.count;
   if (blocks > 0x7fffffffull) return hipErrorNotSupported;
   constexpr uint64_t A = SampleT<InT>::kSrcAlign;
   const bool vec = (reinterpret_cast<uintptr_t>(j.in) % A) == 0 && ((uint64_t)stride * D * sizeof(InT)) % A == 0;
   if (vec) {
-    k_fir_poly_grouped<TapT, InT, D, R, JC, WG, true, MODE, 0, FMB><<<dim3((uint32_t)blocks), dim3(WG), lds, s>>>(
+    k_fir_poly_grouped<TapT, InT, D, R, JC, WG, true, MODE, 0><<<dim3((uint32_t)blocks), dim3(WG), lds, s>>>(
         p, mp, (uint32_t)tiles);
   } else if (shifted_staging<InT>(j.in, (uint64_t)stride * D)) {
-    k_fir_poly_grouped<TapT, InT, D, R, JC, WG, false, MODE, 1, FMB><<<dim3((uint32_t)blocks), dim3(WG), lds, s>>>(
+    k_fir_poly_grouped<TapT, InT, D, R, JC, WG, false, MODE, 1><<<dim3((uint32_t)blocks), dim3(WG), lds, s>>>(
         p, mp, (uint32_t)tiles);
   } else {
-    k_fir_poly_grouped<TapT, InT, D, R, JC, WG, false, MODE, 0, FMB><<<dim3((uint32_t)blocks), dim3(WG), lds, s>>>(
+    k_fir_poly_grouped<TapT, InT, D, R, JC, WG, false, MODE, 0><<<dim3((uint32_t)blocks), dim3(WG), lds, s>>>(
         p, mp, (uint32_t)tiles);
   }
   return launch_status();
@@ -327,7 +328,7 @@ hipError_t launch_multi_chain(const FirJob& j, const MultiParams& mp, hipStream_
     case 2:
       return launch_multi_grouped<float, InT, 2, 8, 16, 128, MODE>(j, mp, s);
     case 4:
-      return launch_multi_grouped<float, InT, 4, 4, 16, 256, MODE, 256>(j, mp, s);
+      return launch_multi_grouped<float, InT, 4, 4, 16, 256, MODE>(j, mp, s);
     case 8:
       return launch_multi_grouped<float, InT, 8, 2, 8, 256, MODE>(j, mp, s);
     default:
@@ -536,17 +537,16 @@ hipError_t launch_poly_d4(const FirJob& j, hipStream_t s) {
     // 2^16 / 2^18 samples 5.41 / 5.51 -> 4.74 / 4.89 us direct, 7.98 / 7.71 -> 5.95 / 5.96 us as a stream call;
     // at 2^20 samples (one such tile a slot) 6.93 -> 8.39 us, so larger calls keep the 512-output tiles
     if (2 * ceil_div<uint64_t>(j.N, 256) <= slots) {
-      return launch_poly<TapT, InT, 4, 1, 16, 256, MODE, 0, true, false, 0, false, 4, 256>(j, s);
+      return launch_poly<TapT, InT, 4, 1, 16, 256, MODE, 0, true, false, 0, false, 4>(j, s);
     }
 #endif
     if (ceil_div<uint64_t>(j.N, 1024) < 3 * slots) {
-      return launch_poly<TapT, InT, 4, 2, 16, 256, MODE, 0, true, false, 0, false, 2, 256>(j, s);
+      return launch_poly<TapT, InT, 4, 2, 16, 256, MODE, 0, true, false, 0, false, 2>(j, s);
     }
   }
-  // (NCO cells of 1,024 outputs and FM partner blocks of 256 for every D = 4 shape, so the three give the same
+  // (one NCO cell grid for every D = 4 shape -- 1,024 outputs for AM, 1,020 for FM -- so the three give the same
   // outputs bit for bit)
-  static_assert(fits_lds_at_t127<InT, 4, 4, 16, 256>(), "default polyphase shape exceeds the LDS budget");
-  return launch_poly<TapT, InT, 4, 4, 16, 256, MODE, 0, true, false, 0, false, 1, 256>(j, s);
+  return launch_poly_default<TapT, InT, 4, 4, 16, 256, MODE>(j, s);
 }
 
 // Runtime-decimation tile kernel (k_fir_rt) for decimations without a compile-time shape, when taps

@@ -708,19 +708,22 @@ __device__ __forceinline__ float4 rel_mix(float4 v, float2 e, float2 w) {
   return make_float4(a.x, a.y, b.x, b.y);
 }
 
-// stage_tile for an anchored chain: row0 = the cell row of the tile's first granule row. Granule g of the tile is
-// row g / WG, lane g % WG of the staging (the same map as stage_tile), so a lane walks its chain one multiply a row.
+// stage_tile for an anchored chain. The tile starts row0 WG - sh granules into its cell (0 <= sh < WG): tile granule
+// g = k WG + tid (the staging map of stage_tile) is cell granule (row0 + k) WG + tid - sh, i.e. lane
+// l = (tid - sh) mod WG of cell row r + k with r = row0, or row0 - 1 for tid < sh. So a thread walks lane l's chain
+// from row r, one multiply a row.
 template <class InT, class Geo, int WG, bool VEC, bool NT, int SH>
 __device__ __forceinline__ void stage_tile_rel(float4* __restrict__ lds, const InT* __restrict__ in, uint64_t S0,
-                                               uint32_t NG, const FirParams& p, uint32_t row0) {
+                                               uint32_t NG, const FirParams& p, uint32_t row0, uint32_t sh) {
   constexpr int G = Geo::G;
   static_assert(G == 2, "NCO modes take complex samples");
   constexpr int BPT = Geo::SG * (Geo::KT / Geo::ROUT) / WG;  // body rows
   static_assert(BPT * WG == Geo::SG * (Geo::KT / Geo::ROUT), "tile body must split evenly over the threads");
   constexpr int SB = staging_batch(BPT);
   const uint32_t tid = threadIdx.x;
+  const uint32_t lane = (tid + WG - sh) % WG, row = row0 - (tid < sh ? 1u : 0u);
   const float2 w = nco_direct(p.nco_inc), F = nco_direct((uint32_t)(2 * WG) * p.nco_inc);
-  float2 e = rel_chain_start<WG>(tid, row0, p.nco_inc);
+  float2 e = rel_chain_start<WG>(lane, row, p.nco_inc);
   if (p.hist != nullptr && (int64_t)S0 + p.in_off < 0) {
     // a streaming call's first tile, which reaches into the stream's history: sample by sample (stream_sample's
     // rule; samples before the call's first window read as zero), 8 rows of loads in flight
@@ -756,14 +759,14 @@ __device__ __forceinline__ void stage_tile_rel(float4* __restrict__ lds, const I
   if constexpr (SH != 0) {
     static_assert(!VEC && SH == 1, "shifted staging is for 8-byte-aligned complex or 2-byte-aligned int8 I/Q input");
     if ((int64_t)S0 + p.in_off >= 1 && S0 + (uint64_t)NG * G <= p.L) {
-      // loaded pair g holds samples 2g - 1 (the odd half of granule g - 1: lane tid - 1's chain, or for lane 0
+      // loaded pair g holds samples 2g - 1 (the odd half of granule g - 1: lane l - 1's chain, or for lane 0
       // lane WG - 1's chain one row behind) and 2g (granule g): the previous lane's chain runs beside this one
-      const uint32_t lp = (tid + WG - 1) % WG;
-      const bool lag = tid == 0 && row0 == 0;  // lane 0 of a cell's first row has no previous granule in the cell
+      const uint32_t lp = (lane + WG - 1) % WG;
+      const bool lag = lane == 0 && row == 0;  // lane 0 of a cell's first row has no previous granule in the cell
       float2 ep = nco_direct((2u * lp) * p.nco_inc);
-      for (uint32_t i = 0; i < row0; ++i) {
+      for (uint32_t i = 0; i < row; ++i) {
         const float2 t = cmul(ep, F);
-        ep = (tid == 0 && i == 0) ? ep : t;  // lane 0 follows lane WG - 1 one row behind
+        ep = (lane == 0 && i == 0) ? ep : t;  // lane 0 follows lane WG - 1 one row behind
       }
       float2* __restrict__ l2 = reinterpret_cast<float2*>(lds);
 #pragma unroll
@@ -798,7 +801,7 @@ __device__ __forceinline__ void stage_tile_rel(float4* __restrict__ lds, const I
           l2[2 * Geo::padded(g)] = b;
         }
       }
-      // the halo (its first granule rewrites the body's last slot whole): granule g of this loop is lane tid - 1's
+      // the halo (its first granule rewrites the body's last slot whole): granule g of this loop is lane l - 1's
       // (lane 0: lane WG - 1's, one row back), i.e. the previous-lane chain's
       for (uint32_t g = BPT * WG - 1 + tid; g < NG; g += WG) {
         ep = cmul(ep, F);
@@ -1005,10 +1008,7 @@ __device__ __forceinline__ bool store_tile_lds(float4* lds, const FirParams& p, 
 
 // Shared by the tiled kernels. `xs` is a WG-sized LDS exchange area (FM mode only); `tile` the staged
 // input tile, which FM mode with COAL reuses (WG * R floats) once every wave is done with it.
-// ANCH (anchored FM tiles, stage_tile_rel): tiles do not overlap and all KT discriminator outputs are written; a
-// thread whose last output's partner starts an FMB-output block takes that partner from xs[WG + b - 1]
-// (fm_block_outputs), every other thread from its neighbour's first output.
-template <int MODE, class OutT, int R, int WG, bool NTS = false, bool COAL = false, bool ANCH = false, int FMB = 1>
+template <int MODE, class OutT, int R, int WG, bool NTS = false, bool COAL = false>
 __device__ __forceinline__ void tile_epilogue(const FirParams& p, uint64_t out0, OutT (&acc)[R], float2* xs,
                                               float4* tile = nullptr) {
   const uint32_t t = threadIdx.x;
@@ -1023,20 +1023,15 @@ __device__ __forceinline__ void tile_epilogue(const FirParams& p, uint64_t out0,
       if (m < p.N) out[m] = am_env(acc[r]);
     }
   } else {
-    // Tiles overlap by one or two FIR outputs (tile_stride = KT - 1 or KT - 2, fm_tile_stride); the
-    // neighbouring thread's first output comes through LDS.
+    // Tiles overlap: the last thread's outputs (anchored polyphase tiles, tile_stride = KT - R) or the last one or
+    // two (the other kernels, KT - 1 or KT - 2, fm_tile_stride) are only partners; the neighbouring thread's
+    // first output comes through LDS.
     xs[t] = acc[0];
     __syncthreads();
     // value select (both loads in range): a select of the two addresses became a flat load through
     // scratch when R = 1
-    float2 nxt;
-    if constexpr (ANCH) {
-      const uint32_t tb = (t + 1) * R;  // tile-local index of the partner
-      nxt = xs[(tb % FMB) == 0 ? WG + tb / FMB - 1 : t + 1];
-    } else {
-      const float2 nb = xs[t + 1 < WG ? t + 1 : t];
-      nxt = (t + 1 < WG) ? nb : acc[R - 1];
-    }
+    const float2 nb = xs[t + 1 < WG ? t + 1 : t];
+    const float2 nxt = (t + 1 < WG) ? nb : acc[R - 1];
     float o[R];
 #pragma unroll
     for (int r = 0; r + 1 < R; r += 2) {
@@ -1252,36 +1247,13 @@ __device__ __forceinline__ uint32_t tile_of_block() {
   }
 }
 
-// Anchored FM tiles: the discriminator partner of an output whose successor starts an FMB-output block. Blocks
-// of FMB outputs (the decimation's smallest tile: 256 at D = 4) tile every tile shape and every NCO cell, and the
-// partner at a block start b FMB is always formed this one way -- in the NCO frame of the output it pairs with,
-// by the wave whose outputs end there, lane-strided over the taps and then a fixed butterfly -- whether it is
-// the next tile's first output, the next cell's, or an output inside this tile; every other partner is the
-// poly core's own output. So a discriminator output is the same value in every tile shape, call split and
-// channel grouping. The products are exactly the reference's (taps below T only). Slot b - 1 of xe.
-template <class TapT, class InT, class Geo, int D, int R, int WG, int FMB>
-__device__ __forceinline__ void fm_block_outputs(const float4* __restrict__ lds, const FirParams& p, float2* xe) {
-  static_assert(FMB % R == 0 && (Geo::KT % FMB) == 0, "blocks of whole threads, whole blocks a tile");
-  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-  const uint32_t tb = (64u * wv + 64u) * R;  // partner index of the wave's last output
-  if (tb % FMB != 0) return;                 // (wave-uniform)
-  const TapT* __restrict__ taps = reinterpret_cast<const TapT*>(p.taps);
-  typename Product<TapT, InT>::type a;
-  set_zero(a);
-  for (uint32_t i = lane; i < p.T; i += 64) mac(a, tile_sample<InT, Geo, true>(lds, tb * D + i), taps[i]);
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) {
-    a.x += __shfl_xor(a.x, m);
-    a.y += __shfl_xor(a.y, m);
-  }
-  if (lane == 0) xe[tb / FMB - 1] = a;
-}
-
 // One tile of the polyphase kernel (the body of k_fir_poly and of k_fir_poly_grouped). FM / AM tiles are
-// anchored (stage_tile_rel): tile t covers outputs [t KT - tile_shift, (t + 1) KT - tile_shift) and is sub-tile
-// (cell_sub0 + t) mod SUBS of its NCO cell of SUBS tiles.
+// anchored (stage_tile_rel): tile t covers outputs [t S - tile_shift, t S - tile_shift + KT) with S = tile_stride
+// (KT for AM; KT - R for FM, whose last thread's outputs only serve as the discriminator partners of the one before,
+// so every discriminator pairs two outputs of one tile in one NCO frame) and is sub-tile (cell_sub0 + t) mod SUBS of
+// its NCO cell of SUBS tiles.
 template <class TapT, class InT, int D, int R, int JC, int WG, bool VEC, int MODE, int ABL, bool NT, int CST, bool DMA,
-          int SH, int SUBS = 1, int FMB = 0>
+          int SH, int SUBS = 1>
 __device__ __forceinline__ void fir_poly_tile(const FirParams& p, uint32_t tile) {
   using Geo = TileGeo<InT, D, R, WG>;
   using OutT = typename Product<TapT, InT>::type;
@@ -1294,21 +1266,25 @@ __device__ __forceinline__ void fir_poly_tile(const FirParams& p, uint32_t tile)
   const HistSample<InT> hist = stream_history_load<InT>(p);
 
   // (an anchored call's first tile may start before output 0: out0 and S0 are then "negative", wrapped)
-  const uint64_t out0 = ANCH ? (uint64_t)tile * Geo::KT - p.tile_shift : (uint64_t)tile * p.tile_stride;
+  const uint64_t out0 = (uint64_t)tile * p.tile_stride - (ANCH ? p.tile_shift : 0u);
   const uint64_t S0 = out0 * D;
   const uint32_t span = p.nch * JC * D;
-  const uint32_t NG = ((MODE == kModeFm ? Geo::KT : Geo::KT - 1) * D + span + G - 1) / G;
-  // LDS: [tile granules | FM exchange (WG float2) | FM block partners (<= 4 float2)]
+  const uint32_t NG = ((Geo::KT - 1) * D + span + G - 1) / G;
+  // LDS: [tile granules | FM exchange (WG float2)]
   constexpr int SMODE = (ABL & 8) ? (int)kModeFir : MODE;
   if constexpr ((ABL & 7) != 2) {
     if constexpr (ANCH && SMODE != kModeFir) {
-      stage_tile_rel<InT, Geo, WG, VEC, NT, SH>(lds, in, S0, NG, p, ((p.cell_sub0 + tile) % SUBS) * BPT);
+      // the tile is sub-tile `sub` of its NCO cell: it starts sub (KT - R) outputs (FM) or sub KT outputs (AM) into
+      // the cell, i.e. sub BPT granule rows in, less sub SG granules for FM (stage_tile_rel)
+      const uint32_t sub = (p.cell_sub0 + tile) % SUBS;
+      stage_tile_rel<InT, Geo, WG, VEC, NT, SH>(lds, in, S0, NG, p, sub * BPT, MODE == kModeFm ? sub * Geo::SG : 0u);
     } else {
       stage_tile<InT, Geo, WG, VEC, SMODE, NT, DMA, SH>(lds, in, S0, NG, p);
     }
   }
   __syncthreads();
   stream_history_store<InT>(p, hist);
+  float2* xs = reinterpret_cast<float2*>(lds + Geo::padded(NG - 1) + 1);
 
   OutT acc[R];
 #pragma unroll
@@ -1323,9 +1299,6 @@ __device__ __forceinline__ void fir_poly_tile(const FirParams& p, uint32_t tile)
       if (!all_finite(acc)) poly_fixup<TapT, InT, D, R, JC, WG>(lds, p, acc);
     }
   }
-  float2* xs = reinterpret_cast<float2*>(lds + Geo::padded(NG - 1) + 1);
-  constexpr int XB = FMB > 0 ? FMB : Geo::KT;  // FM partner blocks (fm_block_outputs)
-  if constexpr (MODE == kModeFm) fm_block_outputs<TapT, InT, Geo, D, R, WG, XB>(lds, p, xs + WG);
 
   if constexpr (CST != 0 && MODE == kModeFir) {
     if (store_tile_lds<CST, OutT, R, WG>(lds, p, out0, acc)) return;
@@ -1339,13 +1312,13 @@ __device__ __forceinline__ void fir_poly_tile(const FirParams& p, uint32_t tile)
     }
     return;
   }
-  tile_epilogue<MODE, OutT, R, WG, NT, true, ANCH, XB>(p, out0, acc, xs, lds);
+  tile_epilogue<MODE, OutT, R, WG, NT, true>(p, out0, acc, xs, lds);
 }
 
 template <class TapT, class InT, int D, int R, int JC, int WG, bool VEC, int MODE, int ABL = 0, bool NT = false,
-          bool XM = false, int CST = 0, bool DMA = false, int SH = 0, int SUBS = 1, int FMB = 0>
+          bool XM = false, int CST = 0, bool DMA = false, int SH = 0, int SUBS = 1>
 __global__ __launch_bounds__(WG) void k_fir_poly(FirParams p) {
-  fir_poly_tile<TapT, InT, D, R, JC, WG, VEC, MODE, ABL, NT, CST, DMA, SH, SUBS, FMB>(p, tile_of_block<XM>());
+  fir_poly_tile<TapT, InT, D, R, JC, WG, VEC, MODE, ABL, NT, CST, DMA, SH, SUBS>(p, tile_of_block<XM>());
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1369,7 +1342,7 @@ struct MultiParams {
 // channel c is bit-identical to gsdrFmDemod / gsdrAmDemod with its own frequency by construction, at
 // the single-channel kernel's register budget. (The first multi-channel kernel read each input tile
 // into registers once and looped over the channels: 228 VGPRs, 2 waves per SIMD, 5 % slower.)
-template <class TapT, class InT, int D, int R, int JC, int WG, bool VEC, int MODE, int SH = 0, int FMB = 0>
+template <class TapT, class InT, int D, int R, int JC, int WG, bool VEC, int MODE, int SH = 0>
 __global__ __launch_bounds__(WG) void k_fir_poly_grouped(FirParams p, MultiParams mp, uint32_t tiles) {
   const uint32_t C = mp.count;
   const uint32_t b = blockIdx.x, r = b >> 3;
@@ -1380,7 +1353,7 @@ __global__ __launch_bounds__(WG) void k_fir_poly_grouped(FirParams p, MultiParam
   pc.fm_gain = mp.gain[c];
   pc.out = reinterpret_cast<float*>(p.out) + (uint64_t)c * mp.out_stride;
   if (c != 0) pc.hist_out = nullptr;  // a multi-channel stream step: channel 0's workgroup 0 copies the history
-  fir_poly_tile<TapT, InT, D, R, JC, WG, VEC, MODE, 0, true, 0, false, SH, 1, FMB>(pc, tile);
+  fir_poly_tile<TapT, InT, D, R, JC, WG, VEC, MODE, 0, true, 0, false, SH, 1>(pc, tile);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1719,14 +1692,12 @@ constexpr size_t mfma_bc_lds_bytes(uint32_t T) {
 // ------------------------------------------------------------------------------------------------
 // Host-side sizing helpers
 // ------------------------------------------------------------------------------------------------
-// (FM: the tile also holds the window of FIR output KT and the exchange area the block partners of the anchored
-// polyphase tiles, fm_block_outputs; the contiguous-window kernels use less)
 template <class InT, int D, int R, int WG>
 constexpr size_t poly_lds_bytes(uint32_t span_samples, int mode) {
   using Geo = TileGeo<InT, D, R, WG>;
-  const uint32_t NG = ((mode == kModeFm ? Geo::KT : Geo::KT - 1) * D + span_samples + Geo::G - 1) / Geo::G;
+  const uint32_t NG = ((Geo::KT - 1) * D + span_samples + Geo::G - 1) / Geo::G;
   size_t bytes = (size_t)(Geo::padded(NG - 1) + 1) * 16u;
-  if (mode != kModeFir) bytes += ((size_t)(WG + 4) * sizeof(float2) + 15) / 16 * 16;
+  if (mode != kModeFir) bytes += ((size_t)WG * sizeof(float2) + 15) / 16 * 16;
   return bytes;
 }
 

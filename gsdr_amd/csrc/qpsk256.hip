@@ -304,60 +304,132 @@ __device__ __forceinline__ void wave_sync() {
 #ifndef GSDR_C256_RECT_LEVELS
 #define GSDR_C256_RECT_LEVELS 0
 #endif
-template <int R3, bool RECT>
-__global__ __launch_bounds__(kCBlock) void k_c256_mod_awgn(const uint8_t* __restrict__ in, float2* __restrict__ out,
+// This lane's six symbols of a step as loaded (a 4-byte and a 2-byte load), kept so until the step needs them:
+// nothing waits for the loads before then.
+struct SymRaw {
+  uint32_t lo;     // symbols 0..3
+  uint32_t hi;     // symbols 4, 5 (low 16 bits)
+  uint32_t shift;  // bytes to drop (the last symbols of the input, loaded from an address moved back)
+};
+
+// The symbols are loaded one step AHEAD: step 0's with the tables, step it + 1's before step it's stores. Vector
+// loads and stores share one in-order counter, so a load issued after a step's stores could only be waited for
+// together with them (an HBM write's whole latency, each step); and issued before the Philox blocks, a step's
+// loads are in flight while they are computed. To keep the compiler's wait counts exact the loads have no branch
+// around them: every lane loads 6 bytes from min(s, n - 6) (so no load leaves the input; unaligned loads are
+// fine on this part) and drops the bytes before s. SMALL (n < 6, chosen by the launcher): byte loads.
+// DEMOD (gsdrxQpsk256ModulateAwgnDemodulate, rectangular table): the same kernel also demodulates every noisy symbol
+// it writes, from the registers that hold it -- the decision of gsdrQpsk256Demodulate's rectangular kernel on the
+// same float values, bit for bit -- and writes the decisions to `dec`: the round trip in one pass, without reading
+// the 134 MB of noisy symbols back.
+template <int R3, bool RECT, bool SMALL, bool DEMOD = false>
+__global__ __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(8))) void k_c256_mod_awgn(const uint8_t* __restrict__ in, float2* __restrict__ out,
                                                             uint32_t n, uint32_t type, float sigma, uint64_t seed,
-                                                            uint64_t firstBlk) {
+                                                            uint64_t firstBlk, uint8_t* __restrict__ dec = nullptr) {
   __shared__ float2 tab[256];
   __shared__ float lev[32];  // RECT: lx[0..15], ly[0..15]
   __shared__ AwgnLds ntab;
   __shared__ float4 stage[kCBlock / 64][kAwgnWaveSyms / 2];  // per wave: 384 symbols as 192 float4
-  awgn_load_table(ntab, kCBlock);
-  if constexpr (RECT) {
-    const float2* src = c_qpsk256_tables[0];
-    if (threadIdx.x < 32) lev[threadIdx.x] = threadIdx.x < 16 ? src[threadIdx.x * 16].x : src[threadIdx.x - 16].y;
-  }
-  load_table(tab, type);  // its barrier publishes the tables
+  __shared__ float levp[DEMOD ? 40 : 1];  // DEMOD: the demodulator's padded level arrays (lxp, lyp; k_c256_demod)
+  float* const lxp = levp;
+  float* const lyp = levp + 20;
   constexpr int NB = R3 == 0 ? 2 : 3;  // Philox blocks touched by six symbols starting at slot R3
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   float4* __restrict__ st = stage[wv];
   // 16-byte aligned output: the wave's stores can be whole float4s (every wave step starts at a multiple
   // of 384 symbols from `out`)
   const bool aligned = (reinterpret_cast<uintptr_t>(out) & 15u) == 0;
-  const bool in_even = (reinterpret_cast<uintptr_t>(in) & 1u) == 0;
   const uint64_t base = (uint64_t)blockIdx.x * kAwgnBlockSyms;
+  auto wave_first = [&](int it) { return base + (uint64_t)kAwgnWaveSyms * ((uint32_t)it * (kCBlock / 64) + wv); };
+  auto load_syms = [&](int it) {
+    SymRaw r;
+    const uint64_t s = wave_first(it) + (uint64_t)kAwgnSym * lane;
+    if constexpr (SMALL) {
+      uint32_t b[kAwgnSym];
+#pragma unroll
+      for (int j = 0; j < kAwgnSym; ++j) b[j] = s + j < n ? in[s + j] : 0u;
+      r.lo = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
+      r.hi = b[4] | (b[5] << 8);
+      r.shift = 0;
+    } else {
+      const uint64_t sl = s < (uint64_t)n - kAwgnSym ? s : (uint64_t)n - kAwgnSym;
+      __builtin_memcpy(&r.lo, in + sl, 4);
+      uint16_t h;
+      __builtin_memcpy(&h, in + sl + 4, 2);
+      r.hi = h;
+      r.shift = (uint32_t)min<uint64_t>(s - sl, kAwgnSym);
+    }
+    return r;
+  };
+  const AwgnRegs treg = awgn_fetch_table();
+  const float2 trow = c_qpsk256_tables[type == 0 ? 0 : 1][threadIdx.x];
+  SymRaw raw = load_syms(0);
+  awgn_store_table(ntab, treg);
+  tab[threadIdx.x] = trow;
+  if constexpr (RECT) {
+    const float2* src = c_qpsk256_tables[0];
+    if (threadIdx.x < 32) lev[threadIdx.x] = threadIdx.x < 16 ? src[threadIdx.x * 16].x : src[threadIdx.x - 16].y;
+  }
+  float lim = -1.0f, scale = 0.0f;
+  if constexpr (DEMOD) {
+    const float2* tsrc = c_qpsk256_tables[0];
+    if (threadIdx.x < 18) {
+      const int k = (int)threadIdx.x - 1;
+      lxp[threadIdx.x] = (k < 0 || k > 15) ? INFINITY : tsrc[k * 16].x;
+      lyp[threadIdx.x] = (k < 0 || k > 15) ? INFINITY : tsrc[k].y;
+    }
+    const float a = tsrc[255].x;  // as k_c256_demod<0>: (15 - 7.5) / 7.5 * a == a exactly
+    scale = 7.5f / a;
+    lim = isfinite(scale) ? 4.0f * fabsf(a) : -1.0f;
+  }
+  __syncthreads();  // publishes the tables
+  // DEMOD: k_c256_demod<0>'s decisions of a lane's six noisy symbols (the reference's cuCabsf argmin, bit for
+  // bit): the quick per-axis decision inline for all six, then -- for the ~1e-4 of symbols within its margin of a
+  // decision boundary, beyond 4|a| or NaN -- the careful path one symbol at a time (unrolled six times over, its
+  // 3 x 3 search had held the kernel at 5 waves a SIMD)
+  auto decide6 = [&](const float2 (&y)[kAwgnSym], uint32_t (&d)[kAwgnSym]) {
+    uint32_t slow = 0;
+#pragma unroll
+    for (int j = 0; j < kAwgnSym; ++j) slow |= demod_rect_quick(y[j], lim, scale, d[j]) ? 0u : 1u << j;
+    if (__builtin_expect(slow != 0, 0)) {
 #pragma unroll 1
-  for (int it = 0; it < kAwgnSteps; ++it) {
-    const uint64_t ws = base + (uint64_t)kAwgnWaveSyms * ((uint32_t)it * (kCBlock / 64) + wv);  // wave's first
-    if (ws >= n) break;
-    const uint64_t s = ws + (uint64_t)kAwgnSym * lane;  // this lane's first symbol (a multiple of 6)
-    const bool whole = ws + kAwgnWaveSyms <= n;          // wave-uniform
+      for (int j = 0; j < kAwgnSym; ++j) {
+        if (!((slow >> j) & 1u)) continue;
+        float2 r = y[0];
+#pragma unroll
+        for (int i = 1; i < kAwgnSym; ++i) r = j == i ? y[i] : r;  // (a select chain: y stays in registers)
+        uint32_t k = demod_rect_fast(lxp, lyp, r, lim, scale);
+        if (k >= 256u) {  // demod_exhaustive's loop, inline: its call (the ABI's saved registers) cost 17 VGPRs
+          float best = INFINITY;
+          k = 0;
+#pragma unroll 1
+          for (uint32_t i = 0; i < 256; ++i) {
+            const float dd = ref_dist(r, tab[i]);
+            if (dd < best) {
+              best = dd;
+              k = i;
+            }
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < kAwgnSym; ++i) d[i] = j == i ? k : d[i];
+      }
+    }
+  };
+  // the noisy symbols of step it (the lane's six, from `raw`)
+  auto step_outputs = [&](int it, float2 (&y)[kAwgnSym]) {
     // (first + s) / 3 with s = base + 384 (it * waves + wv) + 6 lane, every term a multiple of 3
     const uint32_t s3 = (uint32_t)blockIdx.x * (kAwgnBlockSyms / 3u) + (kAwgnWaveSyms / 3u) * ((uint32_t)it * (kCBlock / 64) + wv) +
                         2u * lane;
     const uint64_t b0 = firstBlk + s3;
-    // the main-table normals and outputs of the lane's six symbols
-    auto load_syms = [&](uint8_t (&sym)[kAwgnSym]) {
-      if (whole && in_even) {  // three 2-byte loads (s is even)
-        const uint16_t* __restrict__ in2 = reinterpret_cast<const uint16_t*>(in + s);
-#pragma unroll
-        for (int q = 0; q < kAwgnSym / 2; ++q) {
-          const uint16_t v = in2[q];
-          sym[2 * q] = (uint8_t)v;
-          sym[2 * q + 1] = (uint8_t)(v >> 8);
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < kAwgnSym; ++j) sym[j] = s + j < n ? in[s + j] : 0;
-      }
-    };
-    float2 y[kAwgnSym];
+    uint8_t sym[kAwgnSym];
     {
       uint32_t w[NB][4];
 #pragma unroll
       for (int b = 0; b < NB; ++b) awgn_block_words(seed, b0 + b, w[b]);
-      uint8_t sym[kAwgnSym];
-      load_syms(sym);
+      const uint64_t v6 = ((uint64_t)raw.hi << 32 | raw.lo) >> (8u * raw.shift);
+#pragma unroll
+      for (int j = 0; j < kAwgnSym; ++j) sym[j] = (uint8_t)(v6 >> (8 * j));
 #pragma unroll
       for (int j = 0; j < kAwgnSym; ++j) {
         const float2 g = awgn_slot_main(ntab, w[(R3 + j) / 3], (R3 + j) % 3);
@@ -370,13 +442,11 @@ __global__ __launch_bounds__(kCBlock) void k_c256_mod_awgn(const uint8_t* __rest
       }
     }
     // a lane whose blocks hold a tail component (~4e-4 of the lanes: its outputs hold a NaN, awgn.hpp) redoes
-    // them exactly, regenerating its blocks and reloading its symbols (so neither stays live in the common path)
+    // them exactly, regenerating its blocks (so they do not stay live in the common path)
     if (__builtin_expect(awgn_has_tail(y), 0)) {
       uint32_t w[NB][4];
 #pragma unroll
       for (int b = 0; b < NB; ++b) awgn_block_words(seed, b0 + b, w[b]);
-      uint8_t sym[kAwgnSym];
-      load_syms(sym);
 #pragma unroll
       for (int j = 0; j < kAwgnSym; ++j) {
         const float2 g = awgn_slot(ntab, w[(R3 + j) / 3], (R3 + j) % 3, seed, b0 + (R3 + j) / 3);
@@ -384,20 +454,58 @@ __global__ __launch_bounds__(kCBlock) void k_c256_mod_awgn(const uint8_t* __rest
         y[j] = make_float2(p.x + sigma * g.x, p.y + sigma * g.y);
       }
     }
-    if (whole && aligned) {
+    // the next step's symbols, before this step's stores
+    if (it + 1 < kAwgnSteps) raw = load_syms(it + 1);
+  };
+  // Whole wave steps to an aligned output: a wave's 384 noisy symbols go through LDS so each of its three store
+  // instructions writes 1 KB. (Their own loop: with the per-symbol stores of the other steps in the same loop,
+  // the compiler's wait for the next step's symbols had to cover this step's stores as well.)
+  // Step 0 is peeled off the loop, so that the loop is entered as its back edge enters it -- the next symbols' two
+  // loads, then the three stores -- and the wait for the symbols leaves the stores in flight.
+  auto fast_step = [&](int it) {
+    const uint64_t ws = wave_first(it);  // wave's first
+    float2 y[kAwgnSym];
+    step_outputs(it, y);
 #pragma unroll
-      for (int q = 0; q < kAwgnSym / 2; ++q) {
-        st[lane * 3 + q] = make_float4(y[2 * q].x, y[2 * q].y, y[2 * q + 1].x, y[2 * q + 1].y);
-      }
-      wave_sync();
-      float4* __restrict__ o = reinterpret_cast<float4*>(out + ws);
+    for (int q = 0; q < kAwgnSym / 2; ++q) {
+      st[lane * 3 + q] = make_float4(y[2 * q].x, y[2 * q].y, y[2 * q + 1].x, y[2 * q + 1].y);
+    }
+    wave_sync();
+    float4* __restrict__ o = reinterpret_cast<float4*>(out + ws);
 #pragma unroll
-      for (int q = 0; q < kAwgnSym / 2; ++q) o[q * 64 + lane] = st[q * 64 + lane];
-      wave_sync();  // the next step's LDS writes come after every lane's reads
-    } else {
+    for (int q = 0; q < kAwgnSym / 2; ++q) o[q * 64 + lane] = st[q * 64 + lane];
+    wave_sync();  // the next step's LDS writes come after every lane's reads
+    if constexpr (DEMOD) {  // the lane's six decisions: three 2-byte stores (s even, dec 2-byte aligned)
+      uint32_t d[kAwgnSym];
+      decide6(y, d);
+      uint16_t* __restrict__ d2 = reinterpret_cast<uint16_t*>(dec + ws + (uint64_t)kAwgnSym * lane);
 #pragma unroll
-      for (int j = 0; j < kAwgnSym; ++j) {
-        if (s + j < n) out[s + j] = y[j];
+      for (int q = 0; q < kAwgnSym / 2; ++q) d2[q] = (uint16_t)(d[2 * q] | (d[2 * q + 1] << 8));
+    }
+  };
+  const bool dec_even = !DEMOD || (reinterpret_cast<uintptr_t>(dec) & 1u) == 0;
+  auto fast = [&](int it) { return aligned && dec_even && wave_first(it) + kAwgnWaveSyms <= n; };  // wave-uniform
+  int it = 0;
+  if (fast(0)) {
+    fast_step(0);
+#pragma unroll 1
+    for (it = 1; it < kAwgnSteps && fast(it); ++it) fast_step(it);
+  }
+  // the rest (the input's last, partial wave step; an output only 8-byte aligned): one store a symbol
+#pragma unroll 1
+  for (; it < kAwgnSteps; ++it) {
+    const uint64_t ws = wave_first(it);
+    if (ws >= n) break;
+    const uint64_t s = ws + (uint64_t)kAwgnSym * lane;  // this lane's first symbol (a multiple of 6)
+    float2 y[kAwgnSym];
+    step_outputs(it, y);
+    uint32_t d[kAwgnSym] = {};
+    if constexpr (DEMOD) decide6(y, d);
+#pragma unroll
+    for (int j = 0; j < kAwgnSym; ++j) {
+      if (s + j < n) {
+        out[s + j] = y[j];
+        if constexpr (DEMOD) dec[s + j] = (uint8_t)d[j];
       }
     }
   }
@@ -738,29 +846,37 @@ GSDR_C_LINKAGE hipError_t gsdrQpsk256Modulate(const uint8_t* inputBytes, hipFloa
   return gsdr::c256_launch(true, st, 1, numSymbols, constellationType, cudaDevice, cudaStream);
 }
 
-GSDR_C_LINKAGE hipError_t gsdrxQpsk256ModulateAwgn(const uint8_t* inputBytes, hipFloatComplex* output,
-                                                    uint32_t numSymbols, uint32_t constellationType, float sigma,
-                                                    uint64_t seed, uint64_t firstSymbolIndex, int32_t cudaDevice,
-                                                    hipStream_t cudaStream) GSDR_NO_EXCEPT {
-  if (numSymbols == 0) return hipSuccess;
-  if (inputBytes == nullptr || output == nullptr || !(sigma >= 0.0f) || !(sigma < INFINITY)) {
-    return hipErrorInvalidValue;
-  }
-  gsdr::DeviceScope scope(cudaDevice);
-  if (scope.status() != hipSuccess) return scope.status();
-  const uint32_t blocks = (uint32_t)gsdr::ceil_div<uint64_t>(numSymbols, gsdr::kAwgnBlockSyms);
+namespace gsdr {
+// gsdrxQpsk256ModulateAwgn, and with dec != nullptr the fused round trip of gsdrxQpsk256ModulateAwgnDemodulate
+// (rectangular table only; the caller checks)
+static hipError_t mod_awgn_launch(const uint8_t* inputBytes, hipFloatComplex* output, uint8_t* dec, uint32_t numSymbols,
+                                  uint32_t constellationType, float sigma, uint64_t seed, uint64_t firstSymbolIndex,
+                                  hipStream_t cudaStream) {
+  const uint32_t blocks = (uint32_t)ceil_div<uint64_t>(numSymbols, kAwgnBlockSyms);
   float2* out = reinterpret_cast<float2*>(output);
   const uint64_t blk = firstSymbolIndex / 3u;
-  auto launch = [&](auto r3, auto rect) {
-    gsdr::k_c256_mod_awgn<decltype(r3)::value, decltype(rect)::value><<<dim3(blocks), dim3(gsdr::kCBlock), 0,
-                                                                         cudaStream>>>(
-        inputBytes, out, numSymbols, constellationType, sigma, seed, blk);
+  auto launch = [&](auto r3, auto rect, auto demod) {
+    constexpr int R3 = decltype(r3)::value;
+    constexpr bool RECT = decltype(rect)::value, DEMOD = decltype(demod)::value;
+    if (numSymbols < (uint32_t)kAwgnSym) {
+      k_c256_mod_awgn<R3, RECT, true, DEMOD><<<dim3(blocks), dim3(kCBlock), 0, cudaStream>>>(
+          inputBytes, out, numSymbols, constellationType, sigma, seed, blk, dec);
+    } else {
+      k_c256_mod_awgn<R3, RECT, false, DEMOD><<<dim3(blocks), dim3(kCBlock), 0, cudaStream>>>(
+          inputBytes, out, numSymbols, constellationType, sigma, seed, blk, dec);
+    }
   };
   auto by_type = [&](auto r3) {
-    if (GSDR_C256_RECT_LEVELS && constellationType == 0) {
-      launch(r3, std::true_type{});
+    if (dec != nullptr) {
+      launch(r3, std::false_type{}, std::true_type{});
+    } else if constexpr (GSDR_C256_RECT_LEVELS != 0) {
+      if (constellationType == 0) {
+        launch(r3, std::true_type{}, std::false_type{});
+      } else {
+        launch(r3, std::false_type{}, std::false_type{});
+      }
     } else {
-      launch(r3, std::false_type{});
+      launch(r3, std::false_type{}, std::false_type{});
     }
   };
   switch (firstSymbolIndex % 3u) {
@@ -774,7 +890,44 @@ GSDR_C_LINKAGE hipError_t gsdrxQpsk256ModulateAwgn(const uint8_t* inputBytes, hi
       by_type(std::integral_constant<int, 2>{});
       break;
   }
-  return gsdr::launch_status();
+  return launch_status();
+}
+}  // namespace gsdr
+
+GSDR_C_LINKAGE hipError_t gsdrxQpsk256ModulateAwgn(const uint8_t* inputBytes, hipFloatComplex* output,
+                                                    uint32_t numSymbols, uint32_t constellationType, float sigma,
+                                                    uint64_t seed, uint64_t firstSymbolIndex, int32_t cudaDevice,
+                                                    hipStream_t cudaStream) GSDR_NO_EXCEPT {
+  if (numSymbols == 0) return hipSuccess;
+  if (inputBytes == nullptr || output == nullptr || !(sigma >= 0.0f) || !(sigma < INFINITY)) {
+    return hipErrorInvalidValue;
+  }
+  gsdr::DeviceScope scope(cudaDevice);
+  if (scope.status() != hipSuccess) return scope.status();
+  return gsdr::mod_awgn_launch(inputBytes, output, nullptr, numSymbols, constellationType, sigma, seed, firstSymbolIndex,
+                               cudaStream);
+}
+
+GSDR_C_LINKAGE hipError_t gsdrxQpsk256ModulateAwgnDemodulate(const uint8_t* inputBytes, hipFloatComplex* noisySymbols,
+                                                              uint8_t* outputBytes, uint32_t numSymbols,
+                                                              uint32_t constellationType, float sigma, uint64_t seed,
+                                                              uint64_t firstSymbolIndex, int32_t cudaDevice,
+                                                              hipStream_t cudaStream) GSDR_NO_EXCEPT {
+  if (numSymbols == 0) return hipSuccess;
+  if (inputBytes == nullptr || noisySymbols == nullptr || outputBytes == nullptr || !(sigma >= 0.0f) ||
+      !(sigma < INFINITY)) {
+    return hipErrorInvalidValue;
+  }
+  if (constellationType != 0) {  // circular table: the two calls (the cell lists do not fit beside the AWGN tables)
+    const hipError_t e = gsdrxQpsk256ModulateAwgn(inputBytes, noisySymbols, numSymbols, constellationType, sigma, seed,
+                                                  firstSymbolIndex, cudaDevice, cudaStream);
+    if (e != hipSuccess) return e;
+    return gsdrQpsk256Demodulate(noisySymbols, outputBytes, numSymbols, constellationType, cudaDevice, cudaStream);
+  }
+  gsdr::DeviceScope scope(cudaDevice);
+  if (scope.status() != hipSuccess) return scope.status();
+  return gsdr::mod_awgn_launch(inputBytes, noisySymbols, outputBytes, numSymbols, 0, sigma, seed, firstSymbolIndex,
+                               cudaStream);
 }
 
 GSDR_C_LINKAGE hipError_t gsdrQpsk256Demodulate(const hipFloatComplex* input, uint8_t* outputBytes,

@@ -392,6 +392,22 @@ def qpsk256_modulate_awgn(symbols, constellation_type, sigma, seed, first_symbol
     return out
 
 
+def qpsk256_modulate_awgn_demodulate(symbols, constellation_type, sigma, seed, first_symbol_index=0, noisy=None,
+                                     out=None):
+    """gsdrxQpsk256ModulateAwgnDemodulate: (noisy symbols, decisions) -- exactly gsdrxQpsk256ModulateAwgn then
+    gsdrQpsk256Demodulate, one pass for the rectangular table."""
+    _require(symbols, torch.uint8, "inputBytes")
+    n = symbols.numel()
+    noisy = torch.empty(n, dtype=torch.complex64, device=symbols.device) if noisy is None else noisy
+    out = torch.empty(n, dtype=torch.uint8, device=symbols.device) if out is None else out
+    _require(noisy, torch.complex64, "noisySymbols", n)
+    _require(out, torch.uint8, "outputBytes", n)
+    check("gsdrxQpsk256ModulateAwgnDemodulate",
+          lib.gsdrxQpsk256ModulateAwgnDemodulate(_ptr(symbols), _ptr(noisy), _ptr(out), n, constellation_type, sigma,
+                                                 seed, first_symbol_index, _dev(symbols), stream_of(symbols)))
+    return noisy, out
+
+
 def qpsk256_demodulate(x, constellation_type, out=None):
     _require(x, torch.complex64, "input")
     n = x.numel()

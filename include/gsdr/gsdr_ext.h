@@ -222,4 +222,24 @@ GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxQpsk256ModulateAwgn(
     int32_t cudaDevice,
     hipStream_t cudaStream) GSDR_NO_EXCEPT;
 
+/*
+ * Config 5's whole round trip in one pass: exactly what gsdrxQpsk256ModulateAwgn(inputBytes, noisySymbols, ...)
+ * followed by gsdrQpsk256Demodulate(noisySymbols, outputBytes, numSymbols, constellationType, ...) write --
+ * the same noisy symbols and the same decisions, bit for bit -- but for the rectangular table
+ * (constellationType 0) one kernel demodulates each noisy symbol from the registers it was formed in, so the
+ * noisy buffer is written once and never read back. Other tables run the two calls. Same errors as
+ * gsdrxQpsk256ModulateAwgn, plus hipErrorInvalidValue for a null outputBytes.
+ */
+GSDR_C_LINKAGE GSDR_PUBLIC hipError_t gsdrxQpsk256ModulateAwgnDemodulate(
+    const uint8_t* inputBytes,
+    hipFloatComplex* noisySymbols,
+    uint8_t* outputBytes,
+    uint32_t numSymbols,
+    uint32_t constellationType,
+    float sigma,
+    uint64_t seed,
+    uint64_t firstSymbolIndex,
+    int32_t cudaDevice,
+    hipStream_t cudaStream) GSDR_NO_EXCEPT;
+
 #endif /* GSDR_EXT_H_ */

@@ -428,3 +428,63 @@ def test_qpsk256_rect_quick_path_margin(cuda, amp):
     x = (re.ravel() + 1j * im.ravel()).astype(np.complex64)
     got = ops.qpsk256_demodulate(dev(x, cuda), 0).cpu().numpy()
     assert np.array_equal(got, o.qpsk256_demod(table, x))
+
+
+@pytest.mark.parametrize("n", [1, 5, 6, 7, 385, 4607, 4609, 3 * 4608 + 385, 100_003])
+@pytest.mark.parametrize("first", [0, 1, 2, 2**33 + 3])
+@pytest.mark.parametrize("ctype", [0, 1])
+def test_qpsk256_fused_round_trip_equals_two_calls(cuda, n, first, ctype):
+    """gsdrxQpsk256ModulateAwgnDemodulate writes exactly what gsdrxQpsk256ModulateAwgn followed by
+    gsdrQpsk256Demodulate write: the same noisy symbols and the same decisions, bit for bit (rectangular: one fused
+    kernel; circular: the two calls), at every size (partial waves and workgroups, n < 6) and residue of the first
+    index mod 3; the decisions also equal the oracle's exhaustive cuCabsf argmin on the noisy symbols."""
+    from gsdr_amd import ops
+
+    sigma, seed = (0.05, 0x5EED0005) if ctype == 0 else (0.02, 0xFEED)
+    ops.qpsk256_init(ctype, 1.0)
+    syms_np = np.random.default_rng(n + first).integers(0, 256, n, dtype=np.uint8)
+    syms = dev(syms_np, cuda)
+    rx2 = ops.qpsk256_modulate_awgn(syms, ctype, sigma, seed, first)
+    dec2 = ops.qpsk256_demodulate(rx2, ctype)
+    rx1, dec1 = ops.qpsk256_modulate_awgn_demodulate(syms, ctype, sigma, seed, first)
+    assert rx1.cpu().numpy().tobytes() == rx2.cpu().numpy().tobytes()
+    assert torch.equal(dec1, dec2)
+    table = o.qpsk256_table(ctype, 1.0)
+    assert np.array_equal(dec1.cpu().numpy(), o.qpsk256_demod(table, rx1.cpu().numpy()))
+
+
+@pytest.mark.parametrize("in_off,noisy_off,dec_off", [(1, 0, 0), (0, 1, 0), (0, 0, 1), (1, 1, 1)])
+def test_qpsk256_fused_round_trip_pointer_alignment(cuda, in_off, noisy_off, dec_off):
+    """Odd symbol bytes, noisy symbols 8 bytes off 16-byte alignment, odd decision bytes: the per-symbol path, same
+    bits as the two calls."""
+    from gsdr_amd import ops
+
+    ops.qpsk256_init(0, 1.0)
+    n = 2 * 4608 + 390
+    syms_np = np.random.default_rng(in_off + 2 * noisy_off + 4 * dec_off).integers(0, 256, n + 4, dtype=np.uint8)
+    syms = dev(syms_np, cuda)[in_off:in_off + n]
+    noisy = torch.empty(n + 1, dtype=torch.complex64, device=cuda)[noisy_off:noisy_off + n]
+    dec = torch.empty(n + 1, dtype=torch.uint8, device=cuda)[dec_off:dec_off + n]
+    ops.qpsk256_modulate_awgn_demodulate(syms, 0, 0.03, 77, 11, noisy=noisy, out=dec)
+    rx2 = ops.qpsk256_modulate_awgn(syms, 0, 0.03, 77, 11)
+    assert noisy.cpu().numpy().tobytes() == rx2.cpu().numpy().tobytes()
+    assert torch.equal(dec, ops.qpsk256_demodulate(rx2, 0))
+
+
+def test_qpsk256_fused_config5_bit_exact(cuda):
+    """BASELINE config 5 through the fused entry point: all 2^24 noisy symbols and decisions equal the oracle's
+    (restated channel + exhaustive cuCabsf argmin), and the two-call results."""
+    from gsdr_amd import ops
+
+    n, seed, first, sigma = 1 << 24, 0x5EED_0005, 0, 0.02
+    ops.qpsk256_init(0, 1.0)
+    g = torch.Generator(device=cuda).manual_seed(0x5EED5)
+    syms = torch.randint(0, 256, (n,), dtype=torch.uint8, device=cuda, generator=g)
+    rx, dec = ops.qpsk256_modulate_awgn_demodulate(syms, 0, sigma, seed, first)
+    assert torch.equal(dec, ops.qpsk256_demodulate(rx, 0))
+    table = o.qpsk256_table(0, 1.0)
+    syms_np, rx_np = syms.cpu().numpy(), rx.cpu().numpy()
+    assert rx_np.tobytes() == o.qpsk256_mod_awgn(table, syms_np, sigma, seed, first, nthreads=_threads()).tobytes()
+    assert np.array_equal(dec.cpu().numpy(), o.qpsk256_demod(table, rx_np, nthreads=_threads()))
+    ser = float((dec != syms).float().mean())
+    assert 1e-4 < ser < 1e-2

@@ -231,9 +231,13 @@ __device__ __forceinline__ float2 nco_direct(uint32_t phase) {
 }
 
 // a * b with explicit fmas: (fma(a.x, b.x, -(a.y b.y)), fma(a.x, b.y, a.y b.x)). Written on
-// two-lane vectors so it is exactly one v_pk_mul_f32 (a.y * (-b.y, b.x), the sign as a neg_lo source
-// modifier) and one v_pk_fma_f32 (a.x * b + that); the library builds with -ffp-contract=off, so the
-// rounding is fixed here rather than left to the contraction pass.
+// two-lane vectors so it is one v_pk_mul_f32 (a.y * (-b.y, b.x)) and one v_pk_fma_f32 (a.x * b + that), plus the
+// swapped, negated b (one more v_pk_mul_f32 by (1, -1), hoisted when b is a loop constant); the library builds with
+// -ffp-contract=off, so the rounding is fixed here rather than left to the contraction pass. (Round 6 tried the
+// sign as a neg_lo source modifier of the v_pk_mul_f32, written as inline asm -- the compiler never forms it for
+// packed F32 -- which saves that instruction for every product whose b varies, e.g. each staged granule's NCO mix.
+// An isolated check agreed bit for bit on 2^22 products, but inside the chain kernels the results were wrong (109
+// GPU tests failed), so it is not used.)
 typedef float gsdr_f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
   const gsdr_f32x2 bv = gsdr_f32x2{b.x, b.y};
@@ -1008,6 +1012,32 @@ __device__ __forceinline__ bool store_tile_lds(float4* lds, const FirParams& p, 
 
 // Shared by the tiled kernels. `xs` is a WG-sized LDS exchange area (FM mode only); `tile` the staged
 // input tile, which FM mode with COAL reuses (WG * R floats) once every wave is done with it.
+// A thread's R consecutive demodulated outputs, local indices ml0 .. ml0 + R - 1 of the tile (those below `lim`)
+// at output m0: one 8- or 16-byte store when all R are in range and the address allows, so the lanes of a wave
+// store one contiguous run (R * 256 bytes); one store each otherwise.
+template <int R>
+__device__ __forceinline__ void store_chain(float* __restrict__ out, uint64_t m0, uint32_t ml0, uint32_t lim, uint64_t N,
+                                            const float (&o)[R]) {
+  if constexpr (R == 2 || R == 4) {
+    // (m0 < N first: the anchored tiles' leading outputs have m0 wrapped below zero)
+    if (ml0 + R <= lim && m0 < N && N - m0 >= R && (reinterpret_cast<uintptr_t>(out + m0) % (4 * R)) == 0) {
+      if constexpr (R == 4) {
+        *reinterpret_cast<float4*>(out + m0) = make_float4(o[0], o[1], o[2], o[3]);
+      } else {
+        *reinterpret_cast<float2*>(out + m0) = make_float2(o[0], o[1]);
+      }
+      return;
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    if (ml0 + r < lim && m0 + r < N) out[m0 + r] = o[r];
+  }
+}
+
+// COAL (FM, the contiguous-window kernels' tiles): the discriminator outputs leave through LDS in wave-contiguous
+// runs; without it (the anchored polyphase tiles) each thread stores its R outputs with one vector store
+// (store_chain), which is as contiguous and needs neither the LDS round trip nor its barrier.
 template <int MODE, class OutT, int R, int WG, bool NTS = false, bool COAL = false>
 __device__ __forceinline__ void tile_epilogue(const FirParams& p, uint64_t out0, OutT (&acc)[R], float2* xs,
                                               float4* tile = nullptr) {
@@ -1016,12 +1046,10 @@ __device__ __forceinline__ void tile_epilogue(const FirParams& p, uint64_t out0,
   if constexpr (MODE == kModeFir) {
     store_fir<OutT, R, NTS>(reinterpret_cast<OutT*>(p.out), out0 + local0, p.N, acc);
   } else if constexpr (MODE == kModeAm) {
-    float* out = reinterpret_cast<float*>(p.out);
+    float o[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const uint64_t m = out0 + local0 + r;
-      if (m < p.N) out[m] = am_env(acc[r]);
-    }
+    for (int r = 0; r < R; ++r) o[r] = am_env(acc[r]);
+    store_chain<R>(reinterpret_cast<float*>(p.out), out0 + local0, local0, 0xffffffffu, p.N, o);
   } else {
     // Tiles overlap: the last thread's outputs (anchored polyphase tiles, tile_stride = KT - R) or the last one or
     // two (the other kernels, KT - 1 or KT - 2, fm_tile_stride) are only partners; the neighbouring thread's
@@ -1057,12 +1085,7 @@ __device__ __forceinline__ void tile_epilogue(const FirParams& p, uint64_t out0,
         if (ml < p.tile_stride && m < p.N) out[m] = lo[ml];
       }
     } else {
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const uint32_t ml = local0 + r;
-        const uint64_t m = out0 + ml;
-        if (ml < p.tile_stride && m < p.N) out[m] = o[r];
-      }
+      store_chain<R>(out, out0 + local0, local0, p.tile_stride, p.N, o);
     }
   }
 }
@@ -1312,7 +1335,7 @@ __device__ __forceinline__ void fir_poly_tile(const FirParams& p, uint32_t tile)
     }
     return;
   }
-  tile_epilogue<MODE, OutT, R, WG, NT, true>(p, out0, acc, xs, lds);
+  tile_epilogue<MODE, OutT, R, WG, NT, !ANCH>(p, out0, acc, xs, lds);
 }
 
 template <class TapT, class InT, int D, int R, int JC, int WG, bool VEC, int MODE, int ABL = 0, bool NT = false,

@@ -498,6 +498,48 @@ __device__ __forceinline__ void stream_history_store(const FirParams& p, const H
   }
 }
 
+// The first halo granule of a tile, loaded ahead of the body's loads so that both arrive in one round trip (after
+// the body, it was a second dependent round trip per tile: what a short call's few tiles wait for). The load is
+// one predicated instruction with the raw word(s) kept until the body has been staged: a bounds-checked
+// load_granule there made the compiler wait for it on the spot (its branches merge through register copies).
+template <class InT>
+struct HaloRaw {
+  using type = float4;
+};
+template <>
+struct HaloRaw<Iq8> {
+  using type = uint32_t;
+};
+template <class InT, bool VEC>
+struct HaloPre {
+  typename HaloRaw<InT>::type raw;  // (left undefined when not loaded: a zero there cost a register copy, i.e. a wait)
+  uint64_t s;
+  uint32_t g;
+  bool fast;
+  __device__ __forceinline__ HaloPre(uint64_t S0, uint32_t g0, uint32_t NG, uint64_t L)
+      : s(S0 + (uint64_t)g0 * SampleT<InT>::kPerGranule), g(g0) {
+    fast = VEC && g0 < NG && (int64_t)s >= 0 && s + SampleT<InT>::kPerGranule <= L;
+  }
+  // issued right after the body's first batch of loads (issued before them, it drew a full wait ahead of them)
+  __device__ __forceinline__ void issue(const InT* __restrict__ in) {
+    if (fast) raw = *reinterpret_cast<const typename HaloRaw<InT>::type*>(in + s);
+  }
+  // the granule (only for g < NG). The empty asm re-defines the raw registers here, so the register copies the
+  // allocator makes of the loaded value come after this point and the wait for the load with them, not right
+  // behind the load.
+  __device__ __forceinline__ float4 get(const InT* __restrict__ in, uint64_t L) const {
+    typename HaloRaw<InT>::type r = raw;
+    if constexpr (std::is_same<InT, Iq8>::value) {
+      asm volatile("" : "+v"(r));
+      return fast ? iq8x2_granule(r) : load_granule<InT, VEC>(in, s, L);
+    } else {
+      gsdr_f32x4 q{r.x, r.y, r.z, r.w};
+      asm volatile("" : "+v"(q));
+      return fast ? make_float4(q[0], q[1], q[2], q[3]) : load_granule<InT, VEC>(in, s, L);
+    }
+  }
+};
+
 // SH (complex or int8 I/Q samples): the input is one sample off its aligned granule load (complex: 8 bytes
 // off 16; int8 I/Q: 2 bytes off 4) at every tile start. The tile
 // body is then loaded as aligned 16-byte granules starting one sample early, and each loaded pair is
@@ -622,6 +664,7 @@ __device__ __forceinline__ void stage_tile(float4* __restrict__ lds, const InT* 
       return;
     }
   }
+  HaloPre<InT, VEC> halo(S0, BPT * WG + tid, NG, p.L);
   // The body loop, instantiated once per NCO start parity (`odd` is uniform over the tile): with the
   // parity a runtime value the compiler kept a branch around every granule's phasor.
   const uint32_t pbase = Geo::padded(tid);
@@ -657,6 +700,7 @@ __device__ __forceinline__ void stage_tile(float4* __restrict__ lds, const InT* 
         v[k] = load_granule<InT, VEC>(in, S0 + (uint64_t)((b0 + k) * WG + tid) * G, p.L);
       }
     }
+    if (b0 == 0) halo.issue(in);
 #pragma unroll
     for (int k = 0; k < SB; ++k) {
       const uint32_t g = (b0 + k) * WG + tid;
@@ -674,7 +718,8 @@ __device__ __forceinline__ void stage_tile(float4* __restrict__ lds, const InT* 
   } else {
     body(std::false_type{});
   }
-  for (uint32_t g = BPT * WG + tid; g < NG; g += WG) {
+  if (halo.g < NG) lds[Geo::padded(halo.g)] = stage_transform<InT, MODE>(halo.get(in, p.L), (uint32_t)halo.s, p);
+  for (uint32_t g = halo.g + WG; g < NG; g += WG) {
     const uint64_t s = S0 + (uint64_t)g * G;
     lds[Geo::padded(g)] = stage_transform<InT, MODE>(load_granule<InT, VEC>(in, s, p.L), (uint32_t)s, p);
   }
@@ -818,6 +863,7 @@ __device__ __forceinline__ void stage_tile_rel(float4* __restrict__ lds, const I
   // the last)
   const bool whole = VEC && (int64_t)S0 >= 0 && (S0 + (uint64_t)NG * G <= p.L);
   const uint32_t pbase = Geo::padded(tid);
+  HaloPre<InT, VEC> halo(S0, BPT * WG + tid, NG, p.L);  // (HaloPre)
 #pragma unroll
   for (int b0 = 0; b0 < BPT; b0 += SB) {
     float4 v[SB];
@@ -842,6 +888,7 @@ __device__ __forceinline__ void stage_tile_rel(float4* __restrict__ lds, const I
         v[k] = load_granule<InT, VEC>(in, S0 + (uint64_t)((b0 + k) * WG + tid) * G, p.L);
       }
     }
+    if (b0 == 0) halo.issue(in);
 #pragma unroll
     for (int k = 0; k < SB; ++k) {
       if (b0 + k > 0) e = cmul(e, F);
@@ -850,7 +897,11 @@ __device__ __forceinline__ void stage_tile_rel(float4* __restrict__ lds, const I
       lds[slot] = rel_mix(v[k], e, w);
     }
   }
-  for (uint32_t g = BPT * WG + tid; g < NG; g += WG) {
+  if (halo.g < NG) {
+    e = cmul(e, F);
+    lds[Geo::padded(halo.g)] = rel_mix(halo.get(in, p.L), e, w);
+  }
+  for (uint32_t g = halo.g + WG; g < NG; g += WG) {
     e = cmul(e, F);
     lds[Geo::padded(g)] = rel_mix(load_granule<InT, VEC>(in, S0 + (uint64_t)g * G, p.L), e, w);
   }

@@ -48,7 +48,17 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&x, L * sizeof(hipFloatComplex)));
   CHECK(hipMalloc(&y, (L / D + 4096) * sizeof(float)));
   CHECK(hipMemcpy(dTaps, taps.data(), T * sizeof(float), hipMemcpyHostToDevice));
-  CHECK(hipMemset(x, 0, L * sizeof(hipFloatComplex)));  // the kernels' time does not depend on the values
+  {
+    // a constant-envelope FM signal around the channel (config 3's kind of input; an all-zero input would send
+    // every discriminator output down its atan2f(0, 0) path)
+    std::vector<hipFloatComplex> h(L);
+    double ph = 0.0;
+    for (size_t i = 0; i < L; ++i) {
+      ph += 2 * M_PI * (chan + dev * std::sin(2 * M_PI * 1e3 * (double)i / fs)) / fs;
+      h[i] = make_hipFloatComplex((float)std::cos(ph), (float)std::sin(ph));
+    }
+    CHECK(hipMemcpy(x, h.data(), L * sizeof(hipFloatComplex), hipMemcpyHostToDevice));
+  }
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));

@@ -16,6 +16,7 @@ from gsdr_amd.signals import lowpass_taps  # noqa: E402
 
 ROUNDS = int(os.environ.get("ROUNDS", "4"))
 REPS = int(os.environ.get("REPS", "30"))
+SETTLE = int(os.environ.get("SETTLE", "0"))  # untimed launches before each timed block
 f, u32, i32, p, sz, u64 = ctypes.c_float, ctypes.c_uint32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64
 SIGS = {
     "gsdrFirFC": [sz, p, sz, p, p, sz, i32, p],
@@ -115,7 +116,7 @@ def main():
                 lib = L[li]
                 if name == "config5_fused" and not hasattr(lib, "gsdrxQpsk256ModulateAwgnDemodulate"):
                     continue
-                for k in range(5):
+                for k in range(5 + SETTLE):  # SETTLE: sustained-clock timing like bench.py's (default: short bursts)
                     assert fn(lib, k) == 0
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()

@@ -30,3 +30,19 @@ def test_cpp_example_against_oracle(cuda, tmp_path):
     ref = o.fm_demod(x, taps, 1.0e6, 0.0, 1.0e5, 2.0e4, D, 0, N)
     g = float(np.float32(1.0e6) / (np.float32(2.0) * np.float32(np.pi) * np.float32(2.0e4)))
     assert wrapped_angle_err(fm, ref, g) <= FLOAT_TOL
+
+
+def test_cpp_short_call_timer_runs(cuda):
+    """examples/short_call_timer.cpp: the C++ back-to-back short-call timer runs through the
+    C ABI and reports every shape it times (the numbers themselves are measurements, not asserted)."""
+    import json
+
+    exe = os.path.join(ROOT, "build", "short_call_timer")
+    assert os.path.exists(exe), "build/short_call_timer missing: run `make examples` before the GPU tests"
+    r = subprocess.run([exe, "20"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    d = json.loads(r.stdout)
+    got = {(row["what"], row["samples_per_call"]) for row in d["rows"]}
+    want = {("gsdrMagnitude_256", 256)} | {(w, 1 << s) for w in ("gsdrFmDemod", "gsdrxStreamProcess_fm") for s in (16, 18, 20)}
+    assert got == want, got
+    assert all(row["gpu_us_per_call"] > 0 for row in d["rows"])

@@ -1023,8 +1023,14 @@ __device__ __forceinline__ gsdr_f32x2 fm_disc2(float2 a0, float2 a1, float2 b0, 
 }
 
 // AM envelope: 2 * saturate(|y|) - 1, saturate(NaN) = 0 (reference src/am.cu:49, quad_demod.cu:47-48).
+// |y| as the hardware square root of x^2 + y^2 (within 1 ulp of hypotf, whose library form rescales through a
+// double frexp / ldexp: ~14 instructions an output against ~8). The saturation makes the rescaling moot: a sum
+// that overflows gives +inf where hypotf gives a finite value > 1 (both saturate to 1), one that underflows gives 0
+// where hypotf gives a value below 2^-24 (both give -1); an infinite component gives +inf even beside a NaN, as
+// hypotf does.
 __device__ __forceinline__ float am_env(float2 y) {
-  float m = hypotf(y.x, y.y);
+  float m = __builtin_amdgcn_sqrtf(fmaf(y.x, y.x, y.y * y.y));
+  if (__builtin_isinf(y.x) || __builtin_isinf(y.y)) m = __builtin_inff();
   m = (m > 0.0f) ? (m < 1.0f ? m : 1.0f) : 0.0f;
   return 2.0f * m - 1.0f;
 }

@@ -512,7 +512,10 @@ struct HaloRaw<Iq8> {
 };
 template <class InT, bool VEC>
 struct HaloPre {
-  typename HaloRaw<InT>::type raw;  // (left undefined when not loaded: a zero there cost a register copy, i.e. a wait)
+  // (left indeterminate where nothing is loaded -- get() never returns it then. A zero there, or
+  // __builtin_nondeterministic_value, which the compiler also materialises as zero, cost a register copy right
+  // behind the load, i.e. a wait for it)
+  typename HaloRaw<InT>::type raw;
   uint64_t s;
   uint32_t g;
   bool fast;
